@@ -1,0 +1,310 @@
+// fa_fwd.hip -- kernels, tile-config table, dispatcher and C ABI
+// (include/fa_mi355x.h) of the MI355X flash-attention forward path.
+//
+// Replaces the reference's host dispatcher flash_attention_v9_dispatch and
+// its four template instantiations (flash_attention.cu:606-663), plus the
+// never-launched split-K path (:169-180, :460-496) and its merge kernel
+// flash_attention_splitk_merge (:559-598).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <mutex>
+
+#include "fa_fwd_kernel.hpp"
+#include "fa_mi355x.h"
+
+namespace fa {
+
+// ---------------------------------------------------------------------------
+// workgroup -> (query block, batch*head)
+// ---------------------------------------------------------------------------
+// Causal: heaviest query blocks first (rank 0 = last query block), heads
+// interleaved inside a rank (ref :103-112 does this for S < 2048 only).
+// Non-causal: bijective XCD remap -- workgroups b, b+8, b+16 ... share an XCD,
+// so give each XCD a contiguous run of (head, query block) items: the query
+// blocks of one head then share that XCD's L2 copy of K/V.
+__device__ __forceinline__ void map_block(int id, int nblk, int nqb, int bh_count, bool causal,
+                                          int& qb, int& bh) {
+  if (causal) {
+    const int rank = id / bh_count;
+    bh = id - rank * bh_count;
+    qb = nqb - 1 - rank;
+  } else {
+    const int xcd = id & 7, slot = id >> 3;
+    const int q8 = nblk >> 3, r8 = nblk & 7;
+    const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+    bh = w / nqb;
+    qb = w - bh * nqb;
+  }
+}
+
+template <int WAVES, int BN, bool CAUSAL>
+__global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_kernel(FwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int qb, bh;
+  map_block(blockIdx.x, gridDim.x, p.nqb, p.bh, CAUSAL, qb, bh);
+  attention_tile_loop<WAVES, BN, CAUSAL, false>(p, bh, qb, 0, smem);
+}
+
+// Split-KV: workgroup id -> (split, item); items ordered as map_block.
+template <int WAVES, int BN, bool CAUSAL>
+__global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_splitkv_kernel(FwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int split = blockIdx.x % p.num_splits;
+  const int item = blockIdx.x / p.num_splits;
+  int qb, bh;
+  map_block(item, gridDim.x / p.num_splits, p.nqb, p.bh, CAUSAL, qb, bh);
+  attention_tile_loop<WAVES, BN, CAUSAL, true>(p, bh, qb, split, smem);
+}
+
+// Log-sum-exp merge of split partials (ref flash_attention_splitk_merge,
+// :559-598): one wave per query row, 2 head-dim columns per lane.
+//   M = max_s m_s ; L = sum_s l_s e^(m_s-M) ; O = sum_s O_s e^(m_s-M) / L
+__global__ __launch_bounds__(256) void fa_splitkv_merge_kernel(const float* __restrict__ part_o,
+                                                               const float* __restrict__ part_ml,
+                                                               f16* __restrict__ o, int rows,
+                                                               int num_splits) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float M = -__builtin_inff();
+  for (int s = 0; s < num_splits; ++s) M = fmaxf(M, part_ml[((size_t)s * rows + row) * 2]);
+  float L = 0.f, o0 = 0.f, o1 = 0.f;
+  for (int s = 0; s < num_splits; ++s) {
+    const float2 ml = *reinterpret_cast<const float2*>(part_ml + ((size_t)s * rows + row) * 2);
+    if (ml.y > 0.f) {
+      const float w = __builtin_amdgcn_exp2f((ml.x - M) * 1.4426950408889634f);
+      const float2 po =
+          *reinterpret_cast<const float2*>(part_o + ((size_t)s * rows + row) * HD + 2 * lane);
+      L += ml.y * w;
+      o0 += po.x * w;
+      o1 += po.y * w;
+    }
+  }
+  const float inv = L > 0.f ? 1.0f / L : 0.f;
+  typedef f16 f16x2 __attribute__((ext_vector_type(2)));
+  f16x2 out = {(f16)(o0 * inv), (f16)(o1 * inv)};
+  *reinterpret_cast<f16x2*>(o + (size_t)row * HD + 2 * lane) = out;
+}
+
+// ---------------------------------------------------------------------------
+// config table
+// ---------------------------------------------------------------------------
+typedef void (*kernel_fn)(FwdParams);
+
+struct Config {
+  fa_config_info_t info;
+  kernel_fn fn;
+};
+
+#define FA_CFG(ID, W, BN_, C, SPL, NAME)                                                       \
+  {{ID, 32 * (W), BN_, W, C, SPL, 4 * (BN_) * ROW_BYTES, NAME},                               \
+   SPL ? (kernel_fn)fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0)>                                \
+       : (kernel_fn)fa_fwd_f16_kernel<W, BN_, (C != 0)>}
+
+static const Config kConfigs[] = {
+    FA_CFG(0, 4, 64, 0, 0, "bm128_bn64_w4_noncausal"),
+    FA_CFG(1, 4, 64, 1, 0, "bm128_bn64_w4_causal"),
+    FA_CFG(2, 8, 64, 0, 0, "bm256_bn64_w8_noncausal"),
+    FA_CFG(3, 8, 64, 1, 0, "bm256_bn64_w8_causal"),
+    FA_CFG(4, 8, 128, 0, 0, "bm256_bn128_w8_noncausal"),
+    FA_CFG(5, 8, 128, 1, 0, "bm256_bn128_w8_causal"),
+    FA_CFG(6, 4, 64, 0, 1, "bm128_bn64_w4_noncausal_splitkv"),
+    FA_CFG(7, 4, 64, 1, 1, "bm128_bn64_w4_causal_splitkv"),
+};
+static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
+
+static int prepare(int id) {
+  // raise the dynamic-LDS limit once per config (the reference re-does this
+  // inside every dispatch, :633/641/650/659)
+  static std::once_flag flags[kNumConfigs];
+  static hipError_t errs[kNumConfigs];
+  std::call_once(flags[id], [id] {
+    errs[id] = hipFuncSetAttribute((const void*)kConfigs[id].fn,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   kConfigs[id].info.lds_bytes);
+  });
+  return errs[id] == hipSuccess ? FA_OK : FA_ERR_HIP;
+}
+
+static int check_args(const void* q, const void* k, const void* v, const void* o, int batch,
+                      int heads, int seq_len, int head_dim) {
+  if (batch < 0 || heads < 0 || seq_len < 0 || head_dim < 0) return FA_ERR_BAD_SHAPE;
+  if (head_dim != HD) return FA_ERR_UNSUPPORTED_HEAD_DIM;
+  if ((long long)batch * heads > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
+  if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
+  if (!q || !k || !v || !o) return FA_ERR_NULL_POINTER;
+  return FA_OK;
+}
+
+static int launch(int id, const void* q, const void* k, const void* v, void* o, int bh,
+                  int seq_len, int num_splits, float* part_o, float* part_ml,
+                  hipStream_t stream) {
+  const Config& cfg = kConfigs[id];
+  int rc = prepare(id);
+  if (rc != FA_OK) return rc;
+  FwdParams p;
+  p.q = static_cast<const f16*>(q);
+  p.k = static_cast<const f16*>(k);
+  p.v = static_cast<const f16*>(v);
+  p.o = static_cast<f16*>(o);
+  p.part_o = part_o;
+  p.part_ml = part_ml;
+  p.seq_len = seq_len;
+  p.bh = bh;
+  p.nqb = (seq_len + cfg.info.block_m - 1) / cfg.info.block_m;
+  p.num_splits = num_splits;
+  p.scale = 1.0f / sqrtf((float)HD);          // ref :612
+  p.c = p.scale * 1.4426950408889634f;        // LOG2E, ref :239
+  const long long blocks = (long long)p.nqb * bh * num_splits;
+  if (blocks > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
+  hipLaunchKernelGGL(cfg.fn, dim3((unsigned)blocks), dim3(cfg.info.waves * 64),
+                     cfg.info.lds_bytes, stream, p);
+  return hipGetLastError() == hipSuccess ? FA_OK : FA_ERR_LAUNCH;
+}
+
+static int cfg_for(int waves, int bn, int causal) {
+  for (int i = 0; i < kNumConfigs; ++i)
+    if (kConfigs[i].info.waves == waves && kConfigs[i].info.block_n == bn &&
+        kConfigs[i].info.causal == causal && !kConfigs[i].info.split_kv)
+      return i;
+  return -1;
+}
+
+}  // namespace fa
+
+using namespace fa;
+
+extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
+  // Tier table re-derived for 256 CUs (ref :620-661 picks by seq >= 2048 on
+  // 58 SMs).  256-row workgroups (8 waves) halve the K/V re-reads per query
+  // row; use them once they still give >= 2 workgroups per CU.
+  const long long bh = (long long)batch * heads;
+  const long long wg256 = bh * ((seq_len + 255) / 256);
+  const int waves = wg256 >= 512 ? 8 : 4;
+  return cfg_for(waves, 64, causal ? 1 : 0);
+}
+
+extern "C" int fa_fwd_f16_config(const void* q, const void* k, const void* v, void* o,
+                                 int batch, int heads, int seq_len, int head_dim, int causal,
+                                 int config_id, void* hip_stream) {
+  int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
+  if (rc != FA_OK) return rc;
+  if (config_id < 0 || config_id >= kNumConfigs) return FA_ERR_BAD_CONFIG;
+  const Config& cfg = kConfigs[config_id];
+  if (cfg.info.causal != (causal ? 1 : 0) || cfg.info.split_kv) return FA_ERR_BAD_CONFIG;
+  if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
+  return launch(config_id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
+                (hipStream_t)hip_stream);
+}
+
+extern "C" int fa_fwd_f16(const void* q, const void* k, const void* v, void* o, int batch,
+                          int heads, int seq_len, int head_dim, int causal, void* hip_stream) {
+  int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
+  if (rc != FA_OK) return rc;
+  if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
+  const int id = fa_select_config(batch, heads, seq_len, causal);
+  return launch(id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
+                (hipStream_t)hip_stream);
+}
+
+// ---- split-KV ---------------------------------------------------------------
+static int splitkv_cfg(int causal) { return causal ? 7 : 6; }
+
+extern "C" int fa_splitkv_num_splits(int batch, int heads, int seq_len, int causal) {
+  // enough workgroups to cover 256 CUs twice, at most one split per key tile
+  if (batch <= 0 || heads <= 0 || seq_len <= 0) return 1;
+  const int bm = kConfigs[splitkv_cfg(causal)].info.block_m;
+  const int bn = kConfigs[splitkv_cfg(causal)].info.block_n;
+  const long long items = (long long)batch * heads * ((seq_len + bm - 1) / bm);
+  const int tiles = (seq_len + bn - 1) / bn;
+  long long s = (512 + items - 1) / items;
+  if (s > tiles) s = tiles;
+  if (s > 16) s = 16;
+  return s < 1 ? 1 : (int)s;
+}
+
+extern "C" unsigned long long fa_splitkv_o_bytes(int batch, int heads, int seq_len, int head_dim,
+                                                 int num_splits) {
+  if (batch <= 0 || heads <= 0 || seq_len <= 0 || head_dim <= 0 || num_splits <= 0) return 0;
+  return (unsigned long long)num_splits * batch * heads * seq_len * head_dim * sizeof(float);
+}
+
+extern "C" unsigned long long fa_splitkv_ml_bytes(int batch, int heads, int seq_len, int head_dim,
+                                                  int num_splits) {
+  (void)head_dim;
+  if (batch <= 0 || heads <= 0 || seq_len <= 0 || num_splits <= 0) return 0;
+  return (unsigned long long)num_splits * batch * heads * seq_len * 2 * sizeof(float);
+}
+
+extern "C" int fa_fwd_f16_splitkv(const void* q, const void* k, const void* v, void* o,
+                                  int batch, int heads, int seq_len, int head_dim, int causal,
+                                  int num_splits, float* part_o, float* part_ml,
+                                  void* hip_stream) {
+  int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
+  if (rc != FA_OK) return rc;
+  if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
+  if (num_splits <= 0) num_splits = fa_splitkv_num_splits(batch, heads, seq_len, causal);
+  if (num_splits > 64) return FA_ERR_BAD_CONFIG;
+  if (!part_o || !part_ml) return FA_ERR_WORKSPACE;
+  const int bh = batch * heads;
+  const unsigned long long rows = (unsigned long long)bh * seq_len;
+  if (rows > 0x7fffffffULL) return FA_ERR_BAD_SHAPE;
+  hipStream_t stream = (hipStream_t)hip_stream;
+  rc = launch(splitkv_cfg(causal), q, k, v, o, bh, seq_len, num_splits, part_o, part_ml, stream);
+  if (rc != FA_OK) return rc;
+  hipLaunchKernelGGL(fa_splitkv_merge_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
+                     stream, part_o, part_ml, static_cast<f16*>(o), (int)rows, num_splits);
+  return hipGetLastError() == hipSuccess ? FA_OK : FA_ERR_LAUNCH;
+}
+
+// ---- introspection -----------------------------------------------------------
+extern "C" int fa_num_configs(void) { return kNumConfigs; }
+
+extern "C" int fa_config_info(int config_id, fa_config_info_t* out) {
+  if (config_id < 0 || config_id >= kNumConfigs) return FA_ERR_BAD_CONFIG;
+  if (!out) return FA_ERR_NULL_POINTER;
+  *out = kConfigs[config_id].info;
+  return FA_OK;
+}
+
+extern "C" int fa_kernel_attrs(int config_id, fa_kernel_attrs_t* out) {
+  if (config_id < 0 || config_id >= kNumConfigs) return FA_ERR_BAD_CONFIG;
+  if (!out) return FA_ERR_NULL_POINTER;
+  hipFuncAttributes a;
+  if (hipFuncGetAttributes(&a, (const void*)kConfigs[config_id].fn) != hipSuccess)
+    return FA_ERR_HIP;
+  out->num_regs = a.numRegs;
+  out->local_size_bytes = (int)a.localSizeBytes;
+  out->shared_size_bytes = (int)a.sharedSizeBytes;
+  out->max_threads_per_block = a.maxThreadsPerBlock;
+  out->blocks_per_cu = -1;
+  if (prepare(config_id) == FA_OK) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kConfigs[config_id].fn,
+                                                     kConfigs[config_id].info.waves * 64,
+                                                     kConfigs[config_id].info.lds_bytes) ==
+        hipSuccess)
+      out->blocks_per_cu = nb;
+  }
+  return FA_OK;
+}
+
+extern "C" const char* fa_status_string(int status) {
+  switch (status) {
+    case FA_OK: return "ok";
+    case FA_ERR_NULL_POINTER: return "null device pointer";
+    case FA_ERR_UNSUPPORTED_HEAD_DIM: return "unsupported head_dim (only 128)";
+    case FA_ERR_BAD_SHAPE: return "bad shape";
+    case FA_ERR_LAUNCH: return "kernel launch failed";
+    case FA_ERR_BAD_CONFIG: return "bad tile config";
+    case FA_ERR_HIP: return "HIP runtime error";
+    case FA_ERR_WORKSPACE: return "split-KV buffers missing";
+    default: return "unknown status";
+  }
+}
+
+extern "C" const char* fa_version(void) { return "fa_mi355x 0.1 (gfx950)"; }

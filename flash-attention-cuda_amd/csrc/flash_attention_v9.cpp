@@ -1,0 +1,35 @@
+// flash_attention_v9.cpp -- the reference's C++ dispatcher signature
+// (flash_attention.cu:606-663) on top of the C ABI, with the reference's
+// error convention (CUDA_CHECK -> fprintf + exit(EXIT_FAILURE), :22-30, :662).
+#include "flash_attention_v9.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "fa_mi355x.h"
+
+static void fa_check(int status, const char* file, int line) {
+  if (status != FA_OK) {
+    const hipError_t e = hipGetLastError();
+    fprintf(stderr, "HIP error at %s:%d: %s (%s)\n", file, line, fa_status_string(status),
+            hipGetErrorString(e));
+    exit(EXIT_FAILURE);
+  }
+}
+
+void flash_attention_v9_dispatch(const half* Q, const half* K, const half* V, half* Output,
+                                 float* splitk_buf_O, float* splitk_buf_ml, int batch_size,
+                                 int num_heads, int seq_len, int head_dim, bool causal,
+                                 hipStream_t stream) {
+  if (splitk_buf_O && splitk_buf_ml) {
+    // caller-provided split-K buffers (reference layout, :460-496): run the
+    // split-KV path with the library's split count (fa_splitkv_num_splits)
+    const int rc = fa_fwd_f16_splitkv(Q, K, V, Output, batch_size, num_heads, seq_len, head_dim,
+                                      causal ? 1 : 0, 0, splitk_buf_O, splitk_buf_ml, stream);
+    fa_check(rc, __FILE__, __LINE__);
+    return;
+  }
+  const int rc = fa_fwd_f16(Q, K, V, Output, batch_size, num_heads, seq_len, head_dim,
+                            causal ? 1 : 0, stream);
+  fa_check(rc, __FILE__, __LINE__);
+}

@@ -1,0 +1,292 @@
+"""fa_mi355x -- Python host side of the MI355X flash-attention forward path.
+
+A thin ctypes binding over the C ABI in ``include/fa_mi355x.h`` (the drop-in
+for the reference's ``flash_attention_v9_dispatch``,
+/root/reference/flash_attention.cu:606-663).  PyTorch supplies device memory
+and the current HIP stream; all arithmetic runs in the hand-written gfx950
+kernels of ``libfa_mi355x.so``.  There is no fallback: if the library is
+missing, every entry point raises :class:`FlashAttentionError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import List, Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libfa_mi355x.so")
+
+HEAD_DIM = 128
+
+FA_OK = 0
+FA_ERR_NULL_POINTER = 1
+FA_ERR_UNSUPPORTED_HEAD_DIM = 2
+FA_ERR_BAD_SHAPE = 3
+FA_ERR_LAUNCH = 4
+FA_ERR_BAD_CONFIG = 5
+FA_ERR_HIP = 6
+FA_ERR_WORKSPACE = 7
+
+# every symbol include/fa_mi355x.h declares (tests check the .so exports them)
+EXPORTED_SYMBOLS = (
+    "fa_fwd_f16",
+    "fa_fwd_f16_config",
+    "fa_fwd_f16_splitkv",
+    "fa_splitkv_num_splits",
+    "fa_splitkv_o_bytes",
+    "fa_splitkv_ml_bytes",
+    "fa_select_config",
+    "fa_num_configs",
+    "fa_config_info",
+    "fa_kernel_attrs",
+    "fa_status_string",
+    "fa_version",
+)
+
+
+class FlashAttentionError(RuntimeError):
+    """Raised for a nonzero fa_status_t (the reference exit()s instead)."""
+
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"fa_mi355x error {status}: {msg}")
+        self.status = status
+
+
+class _ConfigInfo(ctypes.Structure):
+    _fields_ = [
+        ("id", ctypes.c_int),
+        ("block_m", ctypes.c_int),
+        ("block_n", ctypes.c_int),
+        ("waves", ctypes.c_int),
+        ("causal", ctypes.c_int),
+        ("split_kv", ctypes.c_int),
+        ("lds_bytes", ctypes.c_int),
+        ("name", ctypes.c_char_p),
+    ]
+
+
+class _KernelAttrs(ctypes.Structure):
+    _fields_ = [
+        ("num_regs", ctypes.c_int),
+        ("local_size_bytes", ctypes.c_int),
+        ("shared_size_bytes", ctypes.c_int),
+        ("max_threads_per_block", ctypes.c_int),
+        ("blocks_per_cu", ctypes.c_int),
+    ]
+
+
+@dataclass(frozen=True)
+class TileConfig:
+    id: int
+    block_m: int
+    block_n: int
+    waves: int
+    causal: bool
+    split_kv: bool
+    lds_bytes: int
+    name: str
+
+
+_lib = None
+
+
+def library_path() -> str:
+    return LIB_PATH
+
+
+def load_library() -> ctypes.CDLL:
+    """Load libfa_mi355x.so (in-tree build). Raises loudly when absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FlashAttentionError(
+            FA_ERR_HIP,
+            f"{LIB_PATH} not built (run `make -C {PKG_ROOT}` or __graft_entry__.build())",
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float)
+    ull = ctypes.c_ulonglong
+    lib.fa_fwd_f16.argtypes = [vp, vp, vp, vp, i, i, i, i, i, vp]
+    lib.fa_fwd_f16.restype = i
+    lib.fa_fwd_f16_config.argtypes = [vp, vp, vp, vp, i, i, i, i, i, i, vp]
+    lib.fa_fwd_f16_config.restype = i
+    lib.fa_fwd_f16_splitkv.argtypes = [vp, vp, vp, vp, i, i, i, i, i, i, vp, vp, vp]
+    lib.fa_fwd_f16_splitkv.restype = i
+    lib.fa_splitkv_num_splits.argtypes = [i, i, i, i]
+    lib.fa_splitkv_num_splits.restype = i
+    lib.fa_splitkv_o_bytes.argtypes = [i, i, i, i, i]
+    lib.fa_splitkv_o_bytes.restype = ull
+    lib.fa_splitkv_ml_bytes.argtypes = [i, i, i, i, i]
+    lib.fa_splitkv_ml_bytes.restype = ull
+    lib.fa_select_config.argtypes = [i, i, i, i]
+    lib.fa_select_config.restype = i
+    lib.fa_num_configs.argtypes = []
+    lib.fa_num_configs.restype = i
+    lib.fa_config_info.argtypes = [i, ctypes.POINTER(_ConfigInfo)]
+    lib.fa_config_info.restype = i
+    lib.fa_kernel_attrs.argtypes = [i, ctypes.POINTER(_KernelAttrs)]
+    lib.fa_kernel_attrs.restype = i
+    lib.fa_status_string.argtypes = [i]
+    lib.fa_status_string.restype = ctypes.c_char_p
+    lib.fa_version.argtypes = []
+    lib.fa_version.restype = ctypes.c_char_p
+    del f
+    _lib = lib
+    return lib
+
+
+def _check(status: int) -> None:
+    if status != FA_OK:
+        msg = load_library().fa_status_string(status).decode()
+        raise FlashAttentionError(status, msg)
+
+
+def version() -> str:
+    return load_library().fa_version().decode()
+
+
+def configs() -> List[TileConfig]:
+    lib = load_library()
+    out = []
+    for cid in range(lib.fa_num_configs()):
+        ci = _ConfigInfo()
+        _check(lib.fa_config_info(cid, ctypes.byref(ci)))
+        out.append(
+            TileConfig(ci.id, ci.block_m, ci.block_n, ci.waves, bool(ci.causal),
+                       bool(ci.split_kv), ci.lds_bytes, ci.name.decode())
+        )
+    return out
+
+
+def select_config(batch: int, heads: int, seq_len: int, causal: bool) -> int:
+    return load_library().fa_select_config(batch, heads, seq_len, int(bool(causal)))
+
+
+def kernel_attrs(config_id: int) -> dict:
+    ka = _KernelAttrs()
+    _check(load_library().fa_kernel_attrs(config_id, ctypes.byref(ka)))
+    return {f: getattr(ka, f) for f, _ in _KernelAttrs._fields_}
+
+
+def _stream_handle(stream) -> Optional[int]:
+    import torch
+
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def _check_qkvo(q, k, v, out):
+    import torch
+
+    for name, t in (("q", q), ("k", k), ("v", v), ("out", out)):
+        if t.dtype != torch.float16:
+            raise FlashAttentionError(FA_ERR_BAD_SHAPE, f"{name} must be float16, got {t.dtype}")
+        if not t.is_cuda:
+            raise FlashAttentionError(FA_ERR_NULL_POINTER, f"{name} must be a device tensor")
+        if not t.is_contiguous():
+            raise FlashAttentionError(FA_ERR_BAD_SHAPE, f"{name} must be contiguous (BHSD)")
+        if t.dim() != 4 or t.shape != q.shape:
+            raise FlashAttentionError(FA_ERR_BAD_SHAPE, f"{name} must be [B,H,S,D] like q")
+
+
+def flash_attention_fwd(q, k, v, causal: bool = False, out=None, config: Optional[int] = None,
+                        stream=None):
+    """O = softmax(Q K^T / sqrt(D) [+ causal mask]) V for fp16 BHSD tensors.
+
+    q, k, v: [batch, heads, seq_len, 128] float16 contiguous device tensors.
+    config: force a tile config id (see :func:`configs`); default = dispatcher.
+    Enqueued on ``stream`` (default: torch's current stream); no sync.
+    """
+    import torch
+
+    if out is None:
+        out = torch.empty_like(q)
+    _check_qkvo(q, k, v, out)
+    b, h, s, d = q.shape
+    lib = load_library()
+    st = ctypes.c_void_p(_stream_handle(stream))
+    args = (ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(k.data_ptr()),
+            ctypes.c_void_p(v.data_ptr()), ctypes.c_void_p(out.data_ptr()), b, h, s, d,
+            int(bool(causal)))
+    if config is None:
+        _check(lib.fa_fwd_f16(*args, st))
+    else:
+        _check(lib.fa_fwd_f16_config(*args, int(config), st))
+    return out
+
+
+def splitkv_buffers(batch: int, heads: int, seq_len: int, num_splits: int, device="cuda"):
+    """Allocate the reference-layout split-K buffers (O partials, (m,l))."""
+    import torch
+
+    rows = batch * heads * seq_len
+    part_o = torch.empty(num_splits * rows * HEAD_DIM, dtype=torch.float32, device=device)
+    part_ml = torch.empty(num_splits * rows * 2, dtype=torch.float32, device=device)
+    return part_o, part_ml
+
+
+def flash_attention_fwd_splitkv(q, k, v, causal: bool = False, num_splits: int = 0, out=None,
+                                part_o=None, part_ml=None, stream=None):
+    """Split-KV forward + log-sum-exp merge (ref split-K path, :169-180/:559-598)."""
+    import torch
+
+    if out is None:
+        out = torch.empty_like(q)
+    _check_qkvo(q, k, v, out)
+    b, h, s, d = q.shape
+    lib = load_library()
+    if num_splits <= 0:
+        num_splits = lib.fa_splitkv_num_splits(b, h, s, int(bool(causal)))
+    if part_o is None or part_ml is None:
+        part_o, part_ml = splitkv_buffers(b, h, s, num_splits, device=q.device)
+    need_o = lib.fa_splitkv_o_bytes(b, h, s, d, num_splits)
+    need_ml = lib.fa_splitkv_ml_bytes(b, h, s, d, num_splits)
+    if part_o.numel() * 4 < need_o or part_ml.numel() * 4 < need_ml:
+        raise FlashAttentionError(FA_ERR_WORKSPACE, "split-KV buffers too small")
+    st = ctypes.c_void_p(_stream_handle(stream))
+    _check(lib.fa_fwd_f16_splitkv(
+        ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(k.data_ptr()),
+        ctypes.c_void_p(v.data_ptr()), ctypes.c_void_p(out.data_ptr()), b, h, s, d,
+        int(bool(causal)), int(num_splits), ctypes.c_void_p(part_o.data_ptr()),
+        ctypes.c_void_p(part_ml.data_ptr()), st))
+    return out
+
+
+def flash_attention_v9_dispatch(Q, K, V, Output, splitk_buf_O, splitk_buf_ml, batch_size: int,
+                                num_heads: int, seq_len: int, head_dim: int, causal: bool,
+                                stream=0):
+    """Mirror of the reference host launch signature (flash_attention.cu:606-611).
+
+    Q/K/V/Output are device tensors (or raw device pointers as ints) holding
+    BHSD fp16 data; splitk_buf_O/splitk_buf_ml may be None (ignored, as the
+    reference does) or reference-layout split-K buffers.  Raises
+    FlashAttentionError where the reference would exit(EXIT_FAILURE).
+    """
+    def ptr(x):
+        if x is None:
+            return None
+        return x if isinstance(x, int) else x.data_ptr()
+
+    lib = load_library()
+    st = ctypes.c_void_p(_stream_handle(stream) if stream not in (0, None) else None)
+    q, k, v, o = (ctypes.c_void_p(ptr(x)) for x in (Q, K, V, Output))
+    if splitk_buf_O is not None and splitk_buf_ml is not None:
+        _check(lib.fa_fwd_f16_splitkv(q, k, v, o, batch_size, num_heads, seq_len, head_dim,
+                                      int(bool(causal)), 0,
+                                      ctypes.c_void_p(ptr(splitk_buf_O)),
+                                      ctypes.c_void_p(ptr(splitk_buf_ml)), st))
+    else:
+        _check(lib.fa_fwd_f16(q, k, v, o, batch_size, num_heads, seq_len, head_dim,
+                              int(bool(causal)), st))
+
+
+def attention_flops(batch: int, heads: int, seq_len: int, head_dim: int, causal: bool) -> float:
+    """Reference FLOP convention: 4*B*H*S^2*D, halved when causal (:938-939)."""
+    f = 4.0 * batch * heads * seq_len * seq_len * head_dim
+    return f / 2 if causal else f

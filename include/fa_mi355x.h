@@ -1,0 +1,115 @@
+/*
+ * fa_mi355x.h -- C ABI of the MI355X (gfx950) flash-attention forward path.
+ *
+ * This is the drop-in boundary for the reference's host dispatcher
+ *   void flash_attention_v9_dispatch(const half* Q, const half* K,
+ *       const half* V, half* Output, float* splitk_buf_O,
+ *       float* splitk_buf_ml, int batch_size, int num_heads, int seq_len,
+ *       int head_dim, bool causal, cudaStream_t stream = 0)
+ * (/root/reference/flash_attention.cu:606-663).  The C++ signature itself is
+ * kept in flash_attention_v9.h and forwards here.
+ *
+ * Conventions shared by every entry point:
+ *  - q, k, v, o are DEVICE pointers owned by the caller (the reference
+ *    allocates them in main, :772-787), fp16 (IEEE binary16), layout BHSD:
+ *    [batch*heads][seq_len][head_dim] contiguous, bh stride seq_len*head_dim
+ *    (:119-122, :672-675).
+ *  - Stream-ordered and non-blocking: the call enqueues on hip_stream (a
+ *    hipStream_t, NULL = default stream) and returns; no allocation, no
+ *    synchronisation, safe to capture into a hipGraph.
+ *  - Return value: FA_OK (0) or a nonzero fa_status_t.  The reference's
+ *    equivalent is CUDA_CHECK(cudaGetLastError()) -> exit (:22-30, :662);
+ *    flash_attention_v9_dispatch() keeps that behaviour on top of this ABI.
+ */
+#ifndef FA_MI355X_H
+#define FA_MI355X_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  FA_OK = 0,
+  FA_ERR_NULL_POINTER = 1,        /* q/k/v/o NULL with a non-empty problem */
+  FA_ERR_UNSUPPORTED_HEAD_DIM = 2,/* only head_dim == 128 (ref :613 HD=128) */
+  FA_ERR_BAD_SHAPE = 3,           /* negative sizes or int overflow of B*H */
+  FA_ERR_LAUNCH = 4,              /* hipGetLastError() after the launch */
+  FA_ERR_BAD_CONFIG = 5,          /* config id out of range / wrong causal */
+  FA_ERR_HIP = 6,                 /* other HIP runtime failure */
+  FA_ERR_WORKSPACE = 7            /* split-KV buffers missing */
+} fa_status_t;
+
+/* Tile configuration descriptor (the reference's template switches
+ * BLOCK_M/BLOCK_N/NWARPS/IS_CAUSAL, :67-70, re-expressed for 64-wide waves). */
+typedef struct {
+  int id;
+  int block_m;      /* query rows per workgroup */
+  int block_n;      /* key/value rows per LDS tile */
+  int waves;        /* 64-lane wavefronts per workgroup */
+  int causal;       /* 1 = causal instantiation */
+  int split_kv;     /* 1 = writes fp32 partials for the LSE merge */
+  int lds_bytes;    /* dynamic LDS per workgroup */
+  const char* name;
+} fa_config_info_t;
+
+/* Per-config compiled resource usage: the reference's register/occupancy
+ * report (cudaFuncGetAttributes + cudaOccupancyMaxActiveBlocksPerMultiprocessor,
+ * :711-755).  Requires a visible GPU for the occupancy field. */
+typedef struct {
+  int num_regs;           /* arch VGPRs per lane (hipFuncAttributes.numRegs) */
+  int local_size_bytes;   /* scratch (spill) bytes per lane */
+  int shared_size_bytes;  /* static LDS */
+  int max_threads_per_block;
+  int blocks_per_cu;      /* occupancy query at the config's LDS size; -1 if no GPU */
+} fa_kernel_attrs_t;
+
+/* Main entry: fused QK^T -> online softmax -> PV forward, fp16 in/out,
+ * fp32 accumulate, scale = 1/sqrt(head_dim) (ref :612).  Chooses the tile
+ * config with fa_select_config(). Replaces flash_attention_v9_dispatch
+ * (flash_attention.cu:606-663). */
+int fa_fwd_f16(const void* q, const void* k, const void* v, void* o,
+               int batch, int heads, int seq_len, int head_dim, int causal,
+               void* hip_stream);
+
+/* Same, forcing one tile config (used to report each (BM,BN,waves) config,
+ * as the reference's bench labels its tiers, :905-916).  The config's causal
+ * flag must equal `causal`. */
+int fa_fwd_f16_config(const void* q, const void* k, const void* v, void* o,
+                      int batch, int heads, int seq_len, int head_dim,
+                      int causal, int config_id, void* hip_stream);
+
+/* Split-KV (flash-decoding) forward: the reference's dead IS_SPLITK path
+ * (:169-180, :460-496) and its merge kernel flash_attention_splitk_merge
+ * (:559-598), made live.  Buffers use the reference's layout:
+ *   part_o  fp32 [num_splits][batch*heads][seq_len][head_dim]  (unnormalised O)
+ *   part_ml fp32 [num_splits][batch*heads][seq_len][2]          (m, l) per row,
+ *           m = running max of the scaled scores (natural-log units, as the
+ *           reference's m_i), l = running sum; an empty split writes (-inf, 0).
+ * num_splits <= 0 uses fa_splitkv_num_splits().  Device buffers are owned by
+ * the caller and must hold fa_splitkv_o_bytes()/fa_splitkv_ml_bytes(). */
+int fa_fwd_f16_splitkv(const void* q, const void* k, const void* v, void* o,
+                       int batch, int heads, int seq_len, int head_dim,
+                       int causal, int num_splits, float* part_o,
+                       float* part_ml, void* hip_stream);
+int fa_splitkv_num_splits(int batch, int heads, int seq_len, int causal);
+unsigned long long fa_splitkv_o_bytes(int batch, int heads, int seq_len,
+                                      int head_dim, int num_splits);
+unsigned long long fa_splitkv_ml_bytes(int batch, int heads, int seq_len,
+                                       int head_dim, int num_splits);
+
+/* The dispatcher's decision (ref tier table :620-661): config id used by
+ * fa_fwd_f16 for this shape. */
+int fa_select_config(int batch, int heads, int seq_len, int causal);
+
+int fa_num_configs(void);
+int fa_config_info(int config_id, fa_config_info_t* out);
+int fa_kernel_attrs(int config_id, fa_kernel_attrs_t* out);
+
+const char* fa_status_string(int status);
+const char* fa_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FA_MI355X_H */
