@@ -1,0 +1,158 @@
+"""CPU tests of the C ABI boundary: the library loads, exports every symbol the
+public headers declare, and the host-side checks/dispatch logic behave -- no
+kernel is launched (no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INCLUDE = os.path.join(ROOT, "include")
+
+
+def _fa():
+    import fa_mi355x
+
+    return fa_mi355x
+
+
+def _declared_functions(header):
+    text = open(os.path.join(INCLUDE, header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"//.*", "", text)
+    # return-type name(  ... ) ;   at file scope (no typedef/struct bodies)
+    names = re.findall(r"^[A-Za-z_][\w \*]*?\b([a-z_][a-z0-9_]*)\s*\([^;{]*\)\s*;", text, re.M)
+    return sorted(set(names))
+
+
+def _dynsyms():
+    lib = _fa().library_path()
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True,
+                         check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_library_loads():
+    fa = _fa()
+    assert os.path.exists(fa.library_path())
+    assert "gfx950" in fa.version()
+
+
+def test_exports_every_c_abi_symbol():
+    declared = _declared_functions("fa_mi355x.h")
+    assert "fa_fwd_f16" in declared and len(declared) >= 10
+    syms = _dynsyms()
+    missing = [d for d in declared if d not in syms]
+    assert not missing, f"declared but not exported: {missing}"
+    assert set(declared) == set(_fa().EXPORTED_SYMBOLS)
+
+
+def test_exports_reference_cpp_signature():
+    declared = _declared_functions("flash_attention_v9.h")
+    assert declared == ["flash_attention_v9_dispatch"]
+    lib = _fa().library_path()
+    out = subprocess.run(["nm", "-DC", "--defined-only", lib], capture_output=True, text=True,
+                         check=True).stdout
+    assert re.search(r"flash_attention_v9_dispatch\(__half const\*, __half const\*, __half const\*,"
+                     r" __half\*, float\*, float\*, int, int, int, int, bool, ihipStream_t\*\)",
+                     out), out
+
+
+def test_config_table():
+    fa = _fa()
+    cfgs = fa.configs()
+    assert [c.id for c in cfgs] == list(range(len(cfgs)))
+    for c in cfgs:
+        assert c.block_m == 32 * c.waves
+        assert c.block_n % 32 == 0
+        assert c.lds_bytes == 4 * c.block_n * 256 <= 160 * 1024
+    # every (waves, bn) non-split config exists for both masks
+    nonsplit = {(c.waves, c.block_n, c.causal) for c in cfgs if not c.split_kv}
+    for w, bn, _ in list(nonsplit):
+        assert (w, bn, True) in nonsplit and (w, bn, False) in nonsplit
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_select_config(causal):
+    fa = _fa()
+    cfgs = fa.configs()
+    for s in (1, 64, 512, 1024, 2048, 4096, 8192, 16384):
+        for b, h in ((1, 32), (64, 32), (8, 32), (1, 1)):
+            cid = fa.select_config(b, h, s, causal)
+            c = cfgs[cid]
+            assert c.causal == causal and not c.split_kv
+
+
+def _null_call(lib, head_dim=128, b=1, h=1, s=64, causal=0, ptr=None):
+    p = ctypes.c_void_p(ptr)
+    return lib.fa_fwd_f16(p, p, p, p, b, h, s, head_dim, causal, None)
+
+
+def test_argument_errors_without_gpu():
+    fa = _fa()
+    lib = fa.load_library()
+    assert _null_call(lib, head_dim=64) == fa.FA_ERR_UNSUPPORTED_HEAD_DIM
+    assert _null_call(lib, head_dim=256) == fa.FA_ERR_UNSUPPORTED_HEAD_DIM
+    assert _null_call(lib, b=-1) == fa.FA_ERR_BAD_SHAPE
+    assert _null_call(lib, s=-5) == fa.FA_ERR_BAD_SHAPE
+    assert _null_call(lib) == fa.FA_ERR_NULL_POINTER
+    assert _null_call(lib, b=0) == fa.FA_OK  # empty problem: nothing to launch
+    assert _null_call(lib, s=0) == fa.FA_OK
+    assert _null_call(lib, b=1 << 16, h=1 << 16) == fa.FA_ERR_BAD_SHAPE
+    p = ctypes.c_void_p(None)
+    q = ctypes.c_void_p(0x1000)  # never dereferenced: every call below fails validation
+    assert lib.fa_fwd_f16_config(q, q, q, q, 1, 1, 64, 128, 0, 999, None) == fa.FA_ERR_BAD_CONFIG
+    # config 0 is non-causal: asking it for causal is rejected before any launch
+    assert lib.fa_fwd_f16_config(q, q, q, q, 1, 1, 64, 128, 1, 0, None) == fa.FA_ERR_BAD_CONFIG
+    assert lib.fa_fwd_f16_splitkv(p, p, p, p, 1, 1, 64, 64, 0, 0, p, p, None) == \
+        fa.FA_ERR_UNSUPPORTED_HEAD_DIM
+    assert lib.fa_fwd_f16_splitkv(q, q, q, q, 1, 1, 64, 128, 0, 2, p, p, None) == \
+        fa.FA_ERR_WORKSPACE
+    assert lib.fa_fwd_f16_splitkv(q, q, q, q, 1, 1, 64, 128, 0, 65, q, q, None) == \
+        fa.FA_ERR_BAD_CONFIG
+
+
+def test_status_strings():
+    lib = _fa().load_library()
+    for st in range(8):
+        assert lib.fa_status_string(st).decode() not in ("", "unknown status")
+    assert lib.fa_status_string(99).decode() == "unknown status"
+
+
+def test_splitkv_sizes():
+    lib = _fa().load_library()
+    assert lib.fa_splitkv_o_bytes(2, 3, 100, 128, 4) == 4 * 2 * 3 * 100 * 128 * 4
+    assert lib.fa_splitkv_ml_bytes(2, 3, 100, 128, 4) == 4 * 2 * 3 * 100 * 2 * 4
+    assert lib.fa_splitkv_o_bytes(0, 3, 100, 128, 4) == 0
+    for s in (1, 64, 1000, 8192):
+        n = lib.fa_splitkv_num_splits(1, 4, s, 1)
+        assert 1 <= n <= 16 and n <= (s + 63) // 64
+
+
+def test_kernel_attrs_needs_runtime():
+    """fa_kernel_attrs reads compiled metadata through the HIP runtime; without a
+    GPU it must fail cleanly (status), never crash."""
+    fa = _fa()
+    try:
+        import torch
+
+        has_gpu = torch.cuda.is_available()
+    except ImportError:
+        has_gpu = False
+    if has_gpu:
+        pytest.skip("GPU present: covered by the gpu tests")
+    with pytest.raises(fa.FlashAttentionError):
+        fa.kernel_attrs(0)
+
+
+def test_python_mirror_rejects_bad_tensors():
+    torch = pytest.importorskip("torch")
+    fa = _fa()
+    x = torch.zeros(1, 1, 8, 128, dtype=torch.float32)
+    with pytest.raises(fa.FlashAttentionError):
+        fa.flash_attention_fwd(x, x, x)
+    y = torch.zeros(1, 1, 8, 128, dtype=torch.float16)  # host tensor
+    with pytest.raises(fa.FlashAttentionError):
+        fa.flash_attention_fwd(y, y, y)
