@@ -10,6 +10,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <mutex>
 
@@ -21,14 +22,36 @@ namespace fa {
 // ---------------------------------------------------------------------------
 // workgroup -> (query block, batch*head)
 // ---------------------------------------------------------------------------
-// Causal: heaviest query blocks first (rank 0 = last query block), heads
-// interleaved inside a rank (ref :103-112 does this for S < 2048 only).
-// Non-causal: bijective XCD remap -- workgroups b, b+8, b+16 ... share an XCD,
-// so give each XCD a contiguous run of (head, query block) items: the query
-// blocks of one head then share that XCD's L2 copy of K/V.
-__device__ __forceinline__ void map_block(int id, int nblk, int nqb, int bh_count, bool causal,
-                                          int& qb, int& bh) {
+// Causal (B*H % 8 == 0): XCD-aware, heaviest-first in "rank bands".  Blocks
+// b, b+8, b+16 ... share an XCD (its own L2); XCD x owns heads x, x+8, ...
+// and walks them heaviest rank band first, the `band` query blocks of one
+// head consecutive inside a band, so co-running blocks on one XCD stream the
+// same K/V tiles through its L2 while load balance stays LPT-like.  (The
+// reference reverses query blocks for S < 2048 only, :103-112.)
+// Otherwise heads are interleaved inside a rank (plain heaviest-first).
+// Non-causal: bijective XCD remap -- each XCD gets a contiguous run of
+// (head, query block) items, so the query blocks of one head share K/V in L2.
+__device__ __forceinline__ void map_block(int id, int nblk, int nqb, int bh_count, int band,
+                                          bool causal, int& qb, int& bh) {
   if (causal) {
+    if ((bh_count & 7) == 0 && nblk == bh_count * nqb && band > 1) {
+      const int x = id & 7, j = id >> 3, hx = bh_count >> 3;
+      const int r = min(nqb, band);
+      const int full = nqb / r, rl = nqb - full * r;
+      int rank, lh;
+      if (j < full * hx * r) {
+        const int bnd = j / (hx * r), k = j - bnd * hx * r;
+        lh = k / r;
+        rank = bnd * r + (k - lh * r);
+      } else {
+        const int k = j - full * hx * r;
+        lh = k / rl;
+        rank = full * r + (k - lh * rl);
+      }
+      bh = x + 8 * lh;
+      qb = nqb - 1 - rank;
+      return;
+    }
     const int rank = id / bh_count;
     bh = id - rank * bh_count;
     qb = nqb - 1 - rank;
@@ -41,23 +64,36 @@ __device__ __forceinline__ void map_block(int id, int nblk, int nqb, int bh_coun
   }
 }
 
-template <int WAVES, int BN, bool CAUSAL>
+// SCHED: 0 = one-barrier-per-tile loop (any wave count), 1 = 8-wave ping-pong
+template <int WAVES, int BN, bool CAUSAL, bool SPLIT, bool USE_M16, int SCHED>
+__device__ __forceinline__ void run_tile_loop(const FwdParams& p, int bh, int qb, int split,
+                                              char* smem) {
+  using Pol = typename std::conditional<USE_M16, M16<BN>, M32<BN>>::type;
+  if constexpr (SCHED == 1) {
+    static_assert(WAVES == 8, "ping-pong needs two groups of four waves");
+    attention_pingpong<Pol, CAUSAL, SPLIT>(p, bh, qb, split, smem);
+  } else {
+    attention_tile_loop<Pol, WAVES, CAUSAL, SPLIT>(p, bh, qb, split, smem);
+  }
+}
+
+template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED>
 __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int qb, bh;
-  map_block(blockIdx.x, gridDim.x, p.nqb, p.bh, CAUSAL, qb, bh);
-  attention_tile_loop<WAVES, BN, CAUSAL, false>(p, bh, qb, 0, smem);
+  map_block(blockIdx.x, gridDim.x, p.nqb, p.bh, p.band, CAUSAL, qb, bh);
+  run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED>(p, bh, qb, 0, smem);
 }
 
 // Split-KV: workgroup id -> (split, item); items ordered as map_block.
-template <int WAVES, int BN, bool CAUSAL>
+template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED>
 __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_splitkv_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int split = blockIdx.x % p.num_splits;
   const int item = blockIdx.x / p.num_splits;
   int qb, bh;
-  map_block(item, gridDim.x / p.num_splits, p.nqb, p.bh, CAUSAL, qb, bh);
-  attention_tile_loop<WAVES, BN, CAUSAL, true>(p, bh, qb, split, smem);
+  map_block(item, gridDim.x / p.num_splits, p.nqb, p.bh, 0, CAUSAL, qb, bh);
+  run_tile_loop<WAVES, BN, CAUSAL, true, USE_M16, SCHED>(p, bh, qb, split, smem);
 }
 
 // Log-sum-exp merge of split partials (ref flash_attention_splitk_merge,
@@ -97,23 +133,38 @@ typedef void (*kernel_fn)(FwdParams);
 
 struct Config {
   fa_config_info_t info;
+  int mfma;   // 32 = v_mfma_f32_32x32x16_f16 loop, 16 = v_mfma_f32_16x16x32_f16 loop
+  int sched;  // 0 = one barrier per tile, 1 = 8-wave ping-pong
   kernel_fn fn;
 };
 
-#define FA_CFG(ID, W, BN_, C, SPL, NAME)                                                       \
-  {{ID, 32 * (W), BN_, W, C, SPL, 4 * (BN_) * ROW_BYTES, NAME},                               \
-   SPL ? (kernel_fn)fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0)>                                \
-       : (kernel_fn)fa_fwd_f16_kernel<W, BN_, (C != 0)>}
+template <int W, int BN_, int C, int SPL, int M, int SCHED>
+constexpr kernel_fn pick_kernel() {
+  if constexpr (SPL)
+    return fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
+  else
+    return fa_fwd_f16_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
+}
+
+#define FA_CFG(ID, W, BN_, C, SPL, M, SCHED, NAME)                                     \
+  {{ID, 32 * (W), BN_, W, C, SPL, 4 * (BN_) * ROW_BYTES, NAME}, M, SCHED, \
+   pick_kernel<W, BN_, C, SPL, M, SCHED>()}
 
 static const Config kConfigs[] = {
-    FA_CFG(0, 4, 64, 0, 0, "bm128_bn64_w4_noncausal"),
-    FA_CFG(1, 4, 64, 1, 0, "bm128_bn64_w4_causal"),
-    FA_CFG(2, 8, 64, 0, 0, "bm256_bn64_w8_noncausal"),
-    FA_CFG(3, 8, 64, 1, 0, "bm256_bn64_w8_causal"),
-    FA_CFG(4, 8, 128, 0, 0, "bm256_bn128_w8_noncausal"),
-    FA_CFG(5, 8, 128, 1, 0, "bm256_bn128_w8_causal"),
-    FA_CFG(6, 4, 64, 0, 1, "bm128_bn64_w4_noncausal_splitkv"),
-    FA_CFG(7, 4, 64, 1, 1, "bm128_bn64_w4_causal_splitkv"),
+    FA_CFG(0, 4, 64, 0, 0, 32, 0, "bm128_bn64_w4_m32_noncausal"),
+    FA_CFG(1, 4, 64, 1, 0, 32, 0, "bm128_bn64_w4_m32_causal"),
+    FA_CFG(2, 8, 64, 0, 0, 32, 0, "bm256_bn64_w8_m32_noncausal"),
+    FA_CFG(3, 8, 64, 1, 0, 32, 0, "bm256_bn64_w8_m32_causal"),
+    FA_CFG(4, 4, 64, 0, 0, 16, 0, "bm128_bn64_w4_m16_noncausal"),
+    FA_CFG(5, 4, 64, 1, 0, 16, 0, "bm128_bn64_w4_m16_causal"),
+    FA_CFG(6, 8, 64, 0, 0, 16, 0, "bm256_bn64_w8_m16_noncausal"),
+    FA_CFG(7, 8, 64, 1, 0, 16, 0, "bm256_bn64_w8_m16_causal"),
+    FA_CFG(8, 8, 64, 0, 0, 16, 1, "bm256_bn64_w8_m16_pingpong_noncausal"),
+    FA_CFG(9, 8, 64, 1, 0, 16, 1, "bm256_bn64_w8_m16_pingpong_causal"),
+    FA_CFG(10, 8, 64, 0, 0, 32, 1, "bm256_bn64_w8_m32_pingpong_noncausal"),
+    FA_CFG(11, 8, 64, 1, 0, 32, 1, "bm256_bn64_w8_m32_pingpong_causal"),
+    FA_CFG(12, 4, 64, 0, 1, 16, 0, "bm128_bn64_w4_m16_noncausal_splitkv"),
+    FA_CFG(13, 4, 64, 1, 1, 16, 0, "bm128_bn64_w4_m16_causal_splitkv"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -128,6 +179,16 @@ static int prepare(int id) {
                                    kConfigs[id].info.lds_bytes);
   });
   return errs[id] == hipSuccess ? FA_OK : FA_ERR_HIP;
+}
+
+// causal rank-band width (query blocks of one head kept together on an XCD);
+// FA_CAUSAL_BAND overrides it for tuning (<= 1 = plain heaviest-first order)
+static int causal_band() {
+  static int band = [] {
+    const char* e = getenv("FA_CAUSAL_BAND");
+    return e ? atoi(e) : 16;
+  }();
+  return band;
 }
 
 static int check_args(const void* q, const void* k, const void* v, const void* o, int batch,
@@ -159,6 +220,7 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   p.num_splits = num_splits;
   p.scale = 1.0f / sqrtf((float)HD);          // ref :612
   p.c = p.scale * 1.4426950408889634f;        // LOG2E, ref :239
+  p.band = causal_band();
   const long long blocks = (long long)p.nqb * bh * num_splits;
   if (blocks > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
   hipLaunchKernelGGL(cfg.fn, dim3((unsigned)blocks), dim3(cfg.info.waves * 64),
@@ -166,10 +228,11 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   return hipGetLastError() == hipSuccess ? FA_OK : FA_ERR_LAUNCH;
 }
 
-static int cfg_for(int waves, int bn, int causal) {
+static int cfg_for(int waves, int bn, int causal, int mfma, int sched) {
   for (int i = 0; i < kNumConfigs; ++i)
     if (kConfigs[i].info.waves == waves && kConfigs[i].info.block_n == bn &&
-        kConfigs[i].info.causal == causal && !kConfigs[i].info.split_kv)
+        kConfigs[i].info.causal == causal && !kConfigs[i].info.split_kv &&
+        kConfigs[i].mfma == mfma && kConfigs[i].sched == sched)
       return i;
   return -1;
 }
@@ -185,7 +248,8 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   const long long bh = (long long)batch * heads;
   const long long wg256 = bh * ((seq_len + 255) / 256);
   const int waves = wg256 >= 512 ? 8 : 4;
-  return cfg_for(waves, 64, causal ? 1 : 0);
+  if (waves == 8) return cfg_for(8, 64, causal ? 1 : 0, 16, 1);  // 16x16x32 ping-pong
+  return cfg_for(4, 64, causal ? 1 : 0, 32, 0);
 }
 
 extern "C" int fa_fwd_f16_config(const void* q, const void* k, const void* v, void* o,
@@ -212,7 +276,7 @@ extern "C" int fa_fwd_f16(const void* q, const void* k, const void* v, void* o, 
 }
 
 // ---- split-KV ---------------------------------------------------------------
-static int splitkv_cfg(int causal) { return causal ? 7 : 6; }
+static int splitkv_cfg(int causal) { return causal ? 13 : 12; }
 
 extern "C" int fa_splitkv_num_splits(int batch, int heads, int seq_len, int causal) {
   // enough workgroups to cover 256 CUs twice, at most one split per key tile

@@ -7,34 +7,38 @@
 // (:103-122 work mapping, :188-334 tile math, :497-553 epilogue).
 //
 // Structure (per wave = 32 query rows, per workgroup = WAVES*32 rows):
-//  * Swapped first product  S^T = K . Q^T  on v_mfma_f32_32x32x16_f16:
-//      A = K tile rows from LDS (ds_read_b128), B = Q held in 32 VGPRs.
-//    The accumulator puts the query on the lane (q = lane&31) and 16 keys in
-//    registers, so the row max / row sum are per-lane scalars plus ONE
-//    cross-half exchange (v_permlane32_swap), no LDS, no shuffles.
+//  * Swapped first product  S^T = K . Q^T : A = K tile rows from LDS
+//    (ds_read_b128), B = Q held in 32 VGPRs for the whole key loop.  The
+//    accumulator puts the query on the lane and keys in registers, so row
+//    max / row sum are per-lane scalars plus cross-row v_permlane*_swap
+//    exchanges -- no LDS round trip, no shuffles.
 //  * Second product  O^T = V^T . P^T : P^T is the first product's accumulator
 //    converted to fp16 in place (B operand, no lane movement); V^T comes from
-//    the row-major V tile in LDS through ds_read_b64_tr_b16 (hardware
-//    transpose read) -- the MI355X replacement for ldmatrix.x2.trans (:305-310).
-//  * One LDS image layout for K and V: 8-row x 32-column subtiles with a
-//    16-byte-chunk XOR (bank-conflict-free for both the b128 row reads and
-//    the tr_b16 column reads; see lds_off()).
-//  * K/V tiles are register-staged and double-buffered in LDS: the global
-//    loads of tile j+1 are issued before tile j's MFMAs and written to the
-//    other LDS buffer after them, one barrier per tile (async-STAGE split).
-//  * Online softmax in the exp2 domain with the scale folded into one FMA,
+//    the row-major V tile through ds_read_b64_tr_b16 (hardware transpose
+//    read) -- the MI355X replacement for ldmatrix.x2.trans (:305-310).
+//  * K/V tiles: raw buffer loads (hardware range check zero-fills rows past
+//    the key range -- no per-lane bounds branches; scalar descriptor math),
+//    register-staged, double-buffered in LDS, one barrier per tile: the loads
+//    of tile j+1 are issued before tile j's MFMAs and written to the other
+//    LDS buffer after them.  The loop is unrolled by two so every LDS address
+//    is a per-lane base + immediate.
+//  * Online softmax in the exp2 domain with the scale folded into one FMA
 //    and a lazy rescale: O and l are rescaled only when some row max grew
-//    by more than RESCALE_LOG2 (P is then bounded by 2^RESCALE_LOG2, exact
-//    in fp16 range), wave-uniform branch.
-//  * Causal: heaviest query blocks launch first (the reference does this
-//    only for S < 2048, :103-112, :643-651; here for every length); waves
-//    skip key tiles that are entirely above their diagonal.
-//  * Non-causal: XCD-aware block remap so the query blocks of one head run
-//    on one XCD and share its L2 copy of K/V.
+//    by more than RESCALE_LOG2 (P stays <= 2^RESCALE_LOG2, exact fp16 range),
+//    wave-uniform branch.
+//  * Causal: waves skip key tiles entirely above their diagonal; the block
+//    ordering (heaviest first, XCD-aware) lives in fa_fwd.hip.
+//
+// Two MFMA shapes share the skeleton (policy classes below):
+//  * M32: v_mfma_f32_32x32x16_f16, one 32-query block per wave.
+//  * M16: v_mfma_f32_16x16x32_f16, two 16-query blocks per wave (the shape
+//    that holds the higher clock under load, profiles/r01_mfma_rate_probe.jsonl).
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 namespace fa {
 
@@ -43,10 +47,12 @@ typedef f16 f16x8 __attribute__((ext_vector_type(8)));
 typedef f16 f16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int HD = 128;           // head_dim (the reference hard-codes 128, :613)
-constexpr int ROW_BYTES = HD * 2; // one K/V/Q row in bytes
+constexpr int HD = 128;            // head_dim (the reference hard-codes 128, :613)
+constexpr int ROW_BYTES = HD * 2;  // one K/V/Q row in bytes
 constexpr float RESCALE_LOG2 = 8.0f;
 
 struct FwdParams {
@@ -62,23 +68,53 @@ struct FwdParams {
   int num_splits;  // key splits (1 = no split)
   float c;         // scale * log2(e)
   float scale;     // 1/sqrt(head_dim)
+  int band;        // causal: query blocks of one head kept together on an XCD
 };
 
-// Byte offset of 16-byte chunk `ch` (0..15) of row `row` in one [rows][128]
-// fp16 tile: 8-row x 32-column subtiles of 512 B, chunk XOR by (row>>2)&3.
+// ---------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes < 0 ? 0 : bytes,
+                                           0x00020000);
+}
+__device__ __forceinline__ f16x8 buf_load16(__amdgpu_buffer_rsrc_t r, int voff) {
+  return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+}
+__device__ __forceinline__ void buf_store8(__amdgpu_buffer_rsrc_t r, int voff, f16x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, 0, 0);
+}
+__device__ __forceinline__ void buf_store16f(__amdgpu_buffer_rsrc_t r, int voff, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, 0, 0);
+}
+
+// LDS image A: 8-row x 32-column subtiles of 512 B, 16-B chunk XOR (row>>2)&3.
+// Conflict-free for ds_read_b64_tr_b16 column reads (both MFMA shapes) and
+// for the 32x32x16 ds_read_b128 row reads.
 __device__ __forceinline__ int lds_off(int row, int ch) {
   return 2048 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) +
          16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
+// LDS image B: plain 256-B rows, chunk XOR (row&15).  Conflict-free for the
+// 16x16x32 ds_read_b128 row reads.
+__device__ __forceinline__ int k_off16(int row, int ch) { return 256 * row + 16 * (ch ^ (row & 15)); }
 
-__device__ __forceinline__ float max_with_partner(float x) {
+__device__ __forceinline__ float max_xor32(float x) {
   // lanes l and l^32 exchange; r[0] = {x[0..31], x[0..31]}, r[1] = {x[32..63], x[32..63]}
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
-__device__ __forceinline__ float sum_with_partner(float x) {
+__device__ __forceinline__ float sum_xor32(float x) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float max_xor16(float x) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+}
+__device__ __forceinline__ float sum_xor16(float x) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(a[0]) + __uint_as_float(a[1]);
 }
 
 __device__ __forceinline__ f16x4 lds_read_tr(const char* base, int off) {
@@ -87,38 +123,425 @@ __device__ __forceinline__ f16x4 lds_read_tr(const char* base, int off) {
   return __builtin_bit_cast(f16x4, t);
 }
 
-// Fill `out` (the key range [kv_lo, kv_hi) of one head) -- the hot loop.
+__device__ __forceinline__ float ninf() { return -__builtin_inff(); }
+
+// ---------------------------------------------------------------------------
+// Policies.  Each holds one wave's state (Q fragments, O accumulator, running
+// max/sum, the current S^T tile and its fp16 P) and splits a key tile into
+//   qk(kb)       : S^T = K . Q^T            (MFMA, K tile from LDS)
+//   softmax(...) : mask, online max/rescale, P = exp2(S*c - m*c), row sums (VALU)
+//   pv(vb)       : O^T += V^T . P^T          (MFMA, V tile from LDS)
+// so the ping-pong skeleton can pair one wave's MFMA block with its SIMD
+// partner's softmax.
+//
+// M32: v_mfma_f32_32x32x16_f16, one 32-query block per wave
+//   S^T[cb] (32 keys x 32 q): lane holds q = lane&31, keys 32cb+(i&3)+8(i>>2)+4h
+//   O^T[e]  (32 d x 32 q):   lane holds q = lane&31, d = 32e+(i&3)+8(i>>2)+4h
+// Both tiles use LDS image A.
+// ---------------------------------------------------------------------------
+template <int BN_>
+struct M32 {
+  static constexpr int BN = BN_;
+  static constexpr int NSB = BN / 32;  // 32-key S^T blocks per tile
+  int lane, r, h;
+  int kaddr0, kaddr1, vaddr0, vaddr1;
+  f16x8 qf[8];
+  f32x16 acc[4];
+  f32x16 s[NSB];
+  f16x8 pf[BN / 16];
+  float m_run, l_run;
+
+  __device__ __forceinline__ void init(int lane_, float /*c*/) {
+    lane = lane_;
+    r = lane & 31;
+    h = lane >> 5;
+    // K row read (A of S^T): row 32cb+r, chunk 2t+h -> 8192cb + 512(t>>1) + kaddr[t&1]
+    kaddr0 = lds_off(r, h);
+    kaddr1 = lds_off(r, 2 + h);
+    // V transposed read (A of O^T): group G=lane>>4, i=lane&15=4qq+pp, rows
+    // 32cb+16s+8m+4h+qq, cols 32e+16(G&1)+4pp -> 8192cb+4096s+512e + vaddr[m]
+    const int G = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
+    const int base = 64 * (4 * h + qq) + 8 * (pp & 1);
+    vaddr0 = base + 16 * ((2 * (G & 1) + (pp >> 1)) ^ h);
+    vaddr1 = 2048 + base + 16 * ((2 * (G & 1) + (pp >> 1)) ^ (2 + h));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] = f32x16{};
+    m_run = ninf();
+    l_run = 0.f;
+  }
+  // Q (B operand of S^T): lane holds Q[qw + r][16t + 8h .. +7]
+  __device__ __forceinline__ void load_q(__amdgpu_buffer_rsrc_t rq, int qw) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) qf[t] = buf_load16(rq, (qw + r) * ROW_BYTES + (2 * t + h) * 16);
+  }
+  // staging: 8 consecutive lanes = two rows of opposite parity x 4 chunks
+  // (conflict-free ds_write_b128 into image A)
+  __device__ __forceinline__ int k_stage_row(int wave) const {
+    return 4 * wave + 2 * ((lane >> 5) & 1) + ((lane >> 2) & 1);
+  }
+  __device__ __forceinline__ int k_stage_ch() const { return 4 * ((lane >> 3) & 3) + (lane & 3); }
+  __device__ __forceinline__ int v_stage_row(int wave) const { return k_stage_row(wave); }
+  __device__ __forceinline__ int v_stage_ch() const { return k_stage_ch(); }
+  static __device__ __forceinline__ int k_lds(int row, int ch) { return lds_off(row, ch); }
+  static __device__ __forceinline__ int v_lds(int row, int ch) { return lds_off(row, ch); }
+
+  __device__ __forceinline__ void qk(const char* kb) {
+#pragma unroll
+    for (int cb = 0; cb < NSB; ++cb) s[cb] = f32x16{};
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int ka = ((t & 1) ? kaddr1 : kaddr0) + 512 * (t >> 1);
+#pragma unroll
+      for (int cb = 0; cb < NSB; ++cb) {
+        const f16x8 kf = *reinterpret_cast<const f16x8*>(kb + ka + 8192 * cb);
+        s[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[t], s[cb], 0, 0, 0);
+      }
+    }
+  }
+  template <bool CAUSAL>
+  __device__ __forceinline__ void softmax(int kv0, int kv_hi, int qw, float c, bool need_mask) {
+    if (need_mask) {
+      const int qrow = qw + r;
+#pragma unroll
+      for (int cb = 0; cb < NSB; ++cb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kv = kv0 + 32 * cb + (i & 3) + 8 * (i >> 2) + 4 * h;
+          const bool ok = kv < kv_hi && (!CAUSAL || kv <= qrow);
+          s[cb][i] = ok ? s[cb][i] : ninf();
+        }
+    }
+    float mx = s[0][0];
+#pragma unroll
+    for (int cb = 0; cb < NSB; ++cb)
+#pragma unroll
+      for (int i = (cb == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, s[cb][i]);
+    mx = max_xor32(mx);
+    const float m_new = fmaxf(m_run, mx);
+    if (__any((m_new - m_run) * c > RESCALE_LOG2)) {
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] *= alpha;
+      l_run *= alpha;
+      m_run = m_new;
+    }
+    // m_run stays -inf only for a row with no visible key yet: keep P = 0, not NaN
+    const float mc = m_run == ninf() ? 0.f : m_run * c;
+    float lsum = 0.f;
+#pragma unroll
+    for (int cb = 0; cb < NSB; ++cb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[cb][i], c, -mc));
+        lsum += pv;
+        pf[2 * cb + (i >> 3)][i & 7] = (f16)pv;
+      }
+    l_run += lsum;
+  }
+  __device__ __forceinline__ void pv(const char* vb) {
+#pragma unroll
+    for (int u = 0; u < BN / 16; ++u) {
+      const int cb = u >> 1, sb = u & 1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int imm = 8192 * cb + 4096 * sb + 512 * e;
+        const f16x4 lo = lds_read_tr(vb, vaddr0 + imm);
+        const f16x4 hi = lds_read_tr(vb, vaddr1 + imm);
+        const f16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        acc[e] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[u], acc[e], 0, 0, 0);
+      }
+    }
+  }
+  template <bool CAUSAL>
+  __device__ __forceinline__ void tile(const char* kb, const char* vb, int kv0, int kv_hi, int qw,
+                                       float c, bool need_mask) {
+    qk(kb);
+    softmax<CAUSAL>(kv0, kv_hi, qw, c, need_mask);
+    pv(vb);
+  }
+
+  // lane holds O^T[d = 32e + (i&3) + 8(i>>2) + 4h][q = qw + r]
+  __device__ __forceinline__ void store_o(__amdgpu_buffer_rsrc_t ro, int qw) {
+    const float lt = sum_xor32(l_run);
+    const float inv = lt > 0.f ? 1.0f / lt : 0.f;
+    const int rowb = (qw + r) * ROW_BYTES;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f16x4 w;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) w[x] = (f16)(acc[e][4 * g + x] * inv);
+        buf_store8(ro, rowb + 2 * (32 * e + 8 * g + 4 * h), w);
+      }
+  }
+  __device__ __forceinline__ void store_partial(__amdgpu_buffer_rsrc_t rpo, float* pml, int qw,
+                                                int S, float scale) {
+    const float lt = sum_xor32(l_run);
+    const int rowb = (qw + r) * HD * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        buf_store16f(rpo, rowb + 4 * (32 * e + 8 * g + 4 * h),
+                     f32x4{acc[e][4 * g], acc[e][4 * g + 1], acc[e][4 * g + 2], acc[e][4 * g + 3]});
+    if (h == 0 && qw + r < S)
+      *reinterpret_cast<float2*>(pml + (size_t)(qw + r) * 2) =
+          make_float2(lt > 0.f ? m_run * scale : ninf(), lt);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// M16: v_mfma_f32_16x16x32_f16, two 16-query blocks b per wave
+//   S^T[b][c] (16 keys x 16 q): lane holds q = 16b + (lane&15),
+//       keys 16c + 4*sg + i, g = lane>>4, sg = swap2(g) -- the K rows are
+//       read permuted (sigma) so the PV transposed reads of one 32-lane half
+//       hit rows 8 apart: bank-conflict-free in image A.
+//   O^T[b][e] (16 d x 16 q):  lane holds q = 16b + (lane&15), d = 16e + 4g + i
+// K tile: image B (conflict-free 16x16x32 row reads); V tile: image A.
+//
+// Softmax (the reference's online softmax, flash_attention.cu:235-288, in the
+// exp2 domain) with two VALU passes moved onto the matrix pipe:
+//  * Q is pre-scaled once by c = scale*log2(e) (fp16), and every QK^T MFMA
+//    chain starts from C = -m_ref (broadcast per query), so the accumulator
+//    already holds x = s*c - m_ref and P = exp2(x) needs no FMA.
+//  * Tile row sums come from one extra MFMA per 32 keys (ones . P): no VALU
+//    adds, and l sums exactly the fp16-rounded P the PV product uses.
+//  * m_ref moves (O and l rescaled) only when a row max grew by more than
+//    RESCALE_LOG2 (wave-uniform branch).
+// ---------------------------------------------------------------------------
+
+template <int BN_>
+struct M16 {
+  static constexpr int BN = BN_;
+  static constexpr int NKB = BN / 16;  // 16-key blocks per tile
+  static constexpr int NU = BN / 32;   // 32-key PV steps per tile
+  int lane, r16, g, sg;
+  int kaddr[4], vaddr[2];
+  f16x8 qf[2][4];
+  f32x4 acc[2][8];
+  f32x4 s[2][NKB];
+  f16x8 pf[2][NU];
+  f32x4 negm[2];     // C operand of the QK^T chains: -m_ref broadcast
+  float m_ref[2];    // reference max, log2 units (x = s*c - m_ref)
+  float l_run[2];
+  bool have_ref;     // wave-uniform: a tile has set m_ref
+  float c;
+
+  __device__ __forceinline__ void init(int lane_, float c_) {
+    lane = lane_;
+    c = c_;
+    r16 = lane & 15;
+    g = lane >> 4;
+    sg = ((g & 1) << 1) | (g >> 1);
+    const int krow = 4 * ((((r16 >> 2) & 1) << 1) | (r16 >> 3)) + (r16 & 3);  // sigma(r16)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) kaddr[t] = k_off16(krow, 4 * t + g);
+    const int i = lane & 15, qq = i >> 2, pp = i & 3;
+#pragma unroll
+    for (int ep = 0; ep < 2; ++ep)
+      vaddr[ep] = 2048 * (sg >> 1) + 64 * (4 * (sg & 1) + qq) + 16 * ((2 * ep + (pp >> 1)) ^ sg) +
+                  8 * (pp & 1);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[b][e] = f32x4{};
+      negm[b] = f32x4{};
+      m_ref[b] = 0.f;
+      l_run[b] = 0.f;
+    }
+    have_ref = false;
+  }
+  // Q: qf[b][t] = c * Q[qw + 16b + r16][32t + 8g .. +7]   (rounded to fp16)
+  __device__ __forceinline__ void load_q(__amdgpu_buffer_rsrc_t rq, int qw) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        f16x8 x = buf_load16(rq, (qw + 16 * b + r16) * ROW_BYTES + (4 * t + g) * 16);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = (f16)((float)x[j] * c);
+        qf[b][t] = x;
+      }
+  }
+  // K staging: natural row-major lanes (8 lanes = 8 chunks of one row: conflict-free
+  // writes into image B); V staging as M32 (image A)
+  __device__ __forceinline__ int k_stage_row(int wave) const { return 4 * wave + (lane >> 4); }
+  __device__ __forceinline__ int k_stage_ch() const { return lane & 15; }
+  __device__ __forceinline__ int v_stage_row(int wave) const {
+    return 4 * wave + 2 * ((lane >> 5) & 1) + ((lane >> 2) & 1);
+  }
+  __device__ __forceinline__ int v_stage_ch() const { return 4 * ((lane >> 3) & 3) + (lane & 3); }
+  static __device__ __forceinline__ int k_lds(int row, int ch) { return k_off16(row, ch); }
+  static __device__ __forceinline__ int v_lds(int row, int ch) { return lds_off(row, ch); }
+
+  __device__ __forceinline__ void qk(const char* kb) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int cb = 0; cb < NKB; ++cb) {
+        const f16x8 kf = *reinterpret_cast<const f16x8*>(kb + kaddr[t] + 4096 * cb);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          s[b][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[b][t], t == 0 ? negm[b] : s[b][cb],
+                                                            0, 0, 0);
+      }
+  }
+  // P = exp2(x) -> fp16 (B operand layout of the PV product), and the tile's
+  // row sums lt[b] (every register of lt[b] holds the sum for q = lane&15)
+  __device__ __forceinline__ void exp_and_sum(f32x4 (&lt)[2]) {
+    const f16x8 ones = {(f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1};
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+      for (int cb = 0; cb < NKB; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          pf[b][cb >> 1][4 * (cb & 1) + i] = (f16)__builtin_amdgcn_exp2f(s[b][cb][i]);
+      lt[b] = f32x4{};
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        lt[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, pf[b][u], lt[b], 0, 0, 0);
+    }
+  }
+  template <bool CAUSAL>
+  __device__ __forceinline__ void softmax(int kv0, int kv_hi, int qw, float /*c*/, bool need_mask) {
+    if (need_mask) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int qrow = qw + 16 * b + r16;
+#pragma unroll
+        for (int cb = 0; cb < NKB; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int kv = kv0 + 16 * cb + 4 * sg + i;
+            const bool ok = kv < kv_hi && (!CAUSAL || kv <= qrow);
+            s[b][cb][i] = ok ? s[b][cb][i] : ninf();
+          }
+      }
+    }
+    // row max relative to m_ref; shift m_ref (and rescale O, l) only when it
+    // grew by more than RESCALE_LOG2 -- P then stays <= 2^RESCALE_LOG2
+    float mx[2];
+    bool grow = !have_ref;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      float m = s[b][0][0];
+#pragma unroll
+      for (int cb = 0; cb < NKB; ++cb)
+#pragma unroll
+        for (int i = (cb == 0 ? 1 : 0); i < 4; ++i) m = fmaxf(m, s[b][cb][i]);
+      mx[b] = max_xor32(max_xor16(m));
+      grow |= mx[b] > RESCALE_LOG2;
+    }
+    if (__any(grow)) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        // first tile: centre on the max; later: only ever move m_ref up.
+        // A row with every key masked (mx = -inf) keeps m_ref.
+        float sh = have_ref ? fmaxf(mx[b], 0.f) : mx[b];
+        sh = sh == ninf() ? 0.f : sh;
+        if (have_ref) {
+          const float alpha = __builtin_amdgcn_exp2f(-sh);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[b][e] *= alpha;
+          l_run[b] *= alpha;
+        }
+#pragma unroll
+        for (int cb = 0; cb < NKB; ++cb) s[b][cb] -= sh;
+        m_ref[b] += sh;
+        negm[b] = f32x4{-m_ref[b], -m_ref[b], -m_ref[b], -m_ref[b]};
+      }
+      have_ref = true;
+    }
+    f32x4 lt[2];
+    exp_and_sum(lt);
+    l_run[0] += lt[0][0];
+    l_run[1] += lt[1][0];
+  }
+  __device__ __forceinline__ void pv(const char* vb) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int base = 8192 * u + 512 * (e >> 1) + vaddr[e & 1];
+        const f16x4 lo = lds_read_tr(vb, base);
+        const f16x4 hi = lds_read_tr(vb, base + 4096);
+        const f16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[b][e] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[b][u], acc[b][e], 0, 0, 0);
+      }
+  }
+  template <bool CAUSAL>
+  __device__ __forceinline__ void tile(const char* kb, const char* vb, int kv0, int kv_hi, int qw,
+                                       float c_, bool need_mask) {
+    qk(kb);
+    softmax<CAUSAL>(kv0, kv_hi, qw, c_, need_mask);
+    pv(vb);
+  }
+
+  __device__ __forceinline__ void store_o(__amdgpu_buffer_rsrc_t ro, int qw) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const float lt = l_run[b];  // already the full row sum (MFMA over all keys)
+      const float inv = lt > 0.f ? 1.0f / lt : 0.f;
+      const int rowb = (qw + 16 * b + r16) * ROW_BYTES;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        f16x4 w;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) w[x] = (f16)(acc[b][e][x] * inv);
+        buf_store8(ro, rowb + 2 * (16 * e + 4 * g), w);
+      }
+    }
+  }
+  // m in the reference's units (scaled score, natural log): m_ref * ln 2
+  __device__ __forceinline__ void store_partial(__amdgpu_buffer_rsrc_t rpo, float* pml, int qw,
+                                                int S, float /*scale*/) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const float lt = l_run[b];
+      const int q = qw + 16 * b + r16;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) buf_store16f(rpo, q * HD * 4 + 4 * (16 * e + 4 * g), acc[b][e]);
+      if (g == 0 && q < S)
+        *reinterpret_cast<float2*>(pml + (size_t)q * 2) =
+            make_float2(lt > 0.f ? m_ref[b] * 0.6931471805599453f : ninf(), lt);
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// The tile loop (shared skeleton)
+//   Pol    : M32<BN> or M16<BN>
 //   WAVES  : 64-lane waves per workgroup (BM = 32*WAVES query rows)
-//   BN     : keys per LDS tile (multiple of 32)
 //   CAUSAL : top-left aligned causal mask (key j visible to query i iff j <= i)
 //   SPLIT  : write unnormalised fp32 O + (m, l) instead of fp16 O
-template <int WAVES, int BN, bool CAUSAL, bool SPLIT>
-__device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, int qb,
-                                                    int split, char* smem) {
-  constexpr int NT = WAVES * 64;                 // threads per workgroup
+// ---------------------------------------------------------------------------
+template <class Pol, int WAVES, bool CAUSAL, bool SPLIT>
+__device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, int qb, int split,
+                                                    char* smem) {
+  constexpr int BN = Pol::BN;
+  constexpr int NT = WAVES * 64;
   constexpr int BM = WAVES * 32;
   constexpr int TILE_BYTES = BN * ROW_BYTES;
-  constexpr int NCH = (BN * 16) / NT;            // 16-B chunks per thread per tile
+  constexpr int NCH = (BN * 16) / NT;  // 16-B chunks per thread per tile (K and V each)
   static_assert((BN * 16) % NT == 0, "tile chunks must divide evenly");
-  static_assert(BN % 32 == 0, "BN multiple of 32");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31;
-  const int h = lane >> 5;
   const int S = p.seq_len;
 
   const size_t head_off = (size_t)bh * (size_t)S * HD;
-  const f16* __restrict__ Qh = p.q + head_off;
-  const f16* __restrict__ Kh = p.k + head_off;
-  const f16* __restrict__ Vh = p.v + head_off;
+  const f16* Qh = p.q + head_off;
+  const f16* Kh = p.k + head_off;
+  const f16* Vh = p.v + head_off;
 
   const int q0 = qb * BM;
-  const int qw = q0 + wave * 32;                 // first query row of this wave
-  const int qrow = qw + r;                       // this lane's query row
+  const int qw = q0 + wave * 32;  // first query row of this wave
 
-  // key range of this workgroup
   int kv_lo = 0, kv_hi = CAUSAL ? min(q0 + BM, S) : S;
   if constexpr (SPLIT) {
     const int ntot = (kv_hi + BN - 1) / BN;
@@ -128,203 +551,211 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
   }
   const int ntiles = kv_hi > kv_lo ? (kv_hi - kv_lo + BN - 1) / BN : 0;
 
-  // ---- Q fragments (B operand of S^T = K.Q^T): lane holds Q[qrow][16t+8h .. +7]
-  f16x8 qf[8];
-  {
-    const f16x8* src = reinterpret_cast<const f16x8*>(Qh + (size_t)qrow * HD);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      f16x8 z = {};
-      qf[t] = qrow < S ? src[2 * t + h] : z;
-    }
-  }
+  Pol pol;
+  pol.init(lane, p.c);
+  pol.load_q(make_rsrc(Qh, S * ROW_BYTES), qw);
 
-  // ---- staging map: chunk (row, ch) handled by this thread for slot i
-  // one wave-instruction covers 4 rows x 256 B; lanes 0-7 hit 8 distinct
-  // 16-B LDS slots (two rows of opposite parity) -> conflict-free ds_write_b128
-  const int st_row0 = 4 * wave + 2 * ((lane >> 5) & 1) + ((lane >> 2) & 1);
-  const int st_ch = 4 * ((lane >> 3) & 3) + (lane & 3);
-  const int st_goff = st_row0 * HD + st_ch * 8;  // element offset inside a tile
-
-  // ---- LDS read addresses (bytes, relative to a tile image)
-  // K row read (A of S^T): row 32c+r, chunk 2t+h -> 8192c + 512(t>>1) + kaddr[t&1]
-  const int kaddr0 = lds_off(r, h);
-  const int kaddr1 = lds_off(r, 2 + h);
-  // V transposed read (A of O^T): group G=lane>>4, i=lane&15=4qq+pp
-  //   rows 32c+16s+8m+4h+qq, cols 32e+16(G&1)+4pp -> 8192c+4096s+512e + vaddr[m]
-  int vaddr0, vaddr1;
-  {
-    const int G = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
-    const int base = 64 * (4 * h + qq) + 8 * (pp & 1);
-    vaddr0 = base + 16 * ((2 * (G & 1) + (pp >> 1)) ^ (h));
-    vaddr1 = 2048 + base + 16 * ((2 * (G & 1) + (pp >> 1)) ^ (2 + h));
-  }
-
+  // staging offsets (compile-time slot i adds 4*WAVES rows)
+  const int kr0 = pol.k_stage_row(wave), kc = pol.k_stage_ch();
+  const int vr0 = pol.v_stage_row(wave), vc = pol.v_stage_ch();
   f16x8 kst[NCH], vst[NCH];
+  // loads of the tile starting at key kv_base; rows at/after kv_hi read as 0
   auto issue_loads = [&](int kv_base) {
-    const f16* kt = Kh + (size_t)kv_base * HD;
-    const f16* vt = Vh + (size_t)kv_base * HD;
+    const int bytes = (kv_hi - kv_base) * ROW_BYTES;
+    const auto rk = make_rsrc(Kh + (size_t)kv_base * HD, bytes);
+    const auto rv = make_rsrc(Vh + (size_t)kv_base * HD, bytes);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int row = st_row0 + 4 * WAVES * i;
-      const int off = st_goff + 4 * WAVES * i * HD;
-      f16x8 z = {};
-      const bool ok = kv_base + row < kv_hi;
-      kst[i] = ok ? *reinterpret_cast<const f16x8*>(kt + off) : z;
-      vst[i] = ok ? *reinterpret_cast<const f16x8*>(vt + off) : z;
+      kst[i] = buf_load16(rk, (kr0 + 4 * WAVES * i) * ROW_BYTES + kc * 16);
+      vst[i] = buf_load16(rv, (vr0 + 4 * WAVES * i) * ROW_BYTES + vc * 16);
     }
   };
-  auto write_lds = [&](int buf) {
-    char* kb = smem + buf * 2 * TILE_BYTES;
+  auto write_lds = [&](char* kb) {
     char* vb = kb + TILE_BYTES;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int off = lds_off(st_row0 + 4 * WAVES * i, st_ch);
-      *reinterpret_cast<f16x8*>(kb + off) = kst[i];
-      *reinterpret_cast<f16x8*>(vb + off) = vst[i];
+      *reinterpret_cast<f16x8*>(kb + Pol::k_lds(kr0 + 4 * WAVES * i, kc)) = kst[i];
+      *reinterpret_cast<f16x8*>(vb + Pol::v_lds(vr0 + 4 * WAVES * i, vc)) = vst[i];
     }
   };
 
-  f32x16 acc[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) acc[e] = f32x16{};
-  float m_run = -__builtin_inff();
-  float l_run = 0.f;
-  const float c = p.c;
-
-  if (ntiles > 0) {
-    issue_loads(kv_lo);
-    write_lds(0);
-  }
+  // prologue: unconditional, so every earlier load (Q included) has retired
+  // before the loop and no in-loop MFMA waits on the prefetch
+  issue_loads(kv_lo);
+  write_lds(smem);
+  // vmcnt(0): the compiler may order the Q loads after the K/V loads; without
+  // this, its waitcnt analysis keeps Q "pending" at the loop header and every
+  // iteration's first MFMAs wait for the in-flight prefetch (vmcnt(N) in QK^T)
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   __syncthreads();
 
-  for (int j = 0; j < ntiles; ++j) {
+  const float c = p.c;
+  auto step = [&](int j, auto buf_c) {
+    constexpr int BUF = decltype(buf_c)::value;
+    char* kb = smem + BUF * 2 * TILE_BYTES;
+    char* kb_next = smem + (BUF ^ 1) * 2 * TILE_BYTES;
     const int kv0 = kv_lo + j * BN;
-    const int buf = j & 1;
-    const bool has_next = j + 1 < ntiles;
-    if (has_next) issue_loads(kv0 + BN);
-
+    issue_loads(kv0 + BN);  // past kv_hi: zero bytes, no memory traffic
     // wave-uniform: does any key of this tile lie at/below some row of this wave?
-    const bool active = !CAUSAL || (kv0 <= qw + 31);
-    if (active) {
-      const char* kb = smem + buf * 2 * TILE_BYTES;
-      const char* vb = kb + TILE_BYTES;
-
-      // ---- S^T = K . Q^T  (BN/32 accumulators of 32 keys x 32 queries)
-      f32x16 s[BN / 32];
-#pragma unroll
-      for (int cb = 0; cb < BN / 32; ++cb) s[cb] = f32x16{};
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int ka = ((t & 1) ? kaddr1 : kaddr0) + 512 * (t >> 1);
-#pragma unroll
-        for (int cb = 0; cb < BN / 32; ++cb) {
-          const f16x8 kf = *reinterpret_cast<const f16x8*>(kb + ka + 8192 * cb);
-          s[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[t], s[cb], 0, 0, 0);
-        }
-      }
-
-      // ---- mask (only tiles that cross the diagonal or the sequence end)
+    if (!CAUSAL || kv0 <= qw + 31) {
       const bool need_mask = (kv0 + BN > kv_hi) || (CAUSAL && kv0 + BN - 1 > qw);
-      if (need_mask) {
-#pragma unroll
-        for (int cb = 0; cb < BN / 32; ++cb) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int kv = kv0 + 32 * cb + (i & 3) + 8 * (i >> 2) + 4 * h;
-            const bool ok = kv < kv_hi && (!CAUSAL || kv <= qrow);
-            s[cb][i] = ok ? s[cb][i] : -__builtin_inff();
-          }
-        }
-      }
-
-      // ---- online softmax (exp2 domain, lazy rescale)
-      float mx = s[0][0];
-#pragma unroll
-      for (int cb = 0; cb < BN / 32; ++cb)
-#pragma unroll
-        for (int i = (cb == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, s[cb][i]);
-      mx = max_with_partner(mx);
-      const float m_new = fmaxf(m_run, mx);
-      if (__any((m_new - m_run) * c > RESCALE_LOG2)) {
-        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] *= alpha;
-        l_run *= alpha;
-        m_run = m_new;
-      }
-      // m_run stays -inf only for a row with no visible key yet: keep P = 0, not NaN
-      const float mc = m_run == -__builtin_inff() ? 0.f : m_run * c;
-
-      f16x8 pf[BN / 16];
-      float lsum = 0.f;
-#pragma unroll
-      for (int cb = 0; cb < BN / 32; ++cb) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[cb][i], c, -mc));
-          lsum += pv;
-          pf[2 * cb + (i >> 3)][i & 7] = (f16)pv;
-        }
-      }
-      l_run += lsum;
-
-      // ---- O^T += V^T . P^T
-#pragma unroll
-      for (int u = 0; u < BN / 16; ++u) {
-        const int cb = u >> 1, sb = u & 1;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int imm = 8192 * cb + 4096 * sb + 512 * e;
-          const f16x4 lo = lds_read_tr(vb, vaddr0 + imm);
-          const f16x4 hi = lds_read_tr(vb, vaddr1 + imm);
-          const f16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-          acc[e] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[u], acc[e], 0, 0, 0);
-        }
-      }
+      pol.template tile<CAUSAL>(kb, kb + TILE_BYTES, kv0, kv_hi, qw, c, need_mask);
     }
+    write_lds(kb_next);
+    __syncthreads();
+  };
+  int j = 0;
+  for (; j + 1 < ntiles; j += 2) {
+    step(j, std::integral_constant<int, 0>{});
+    step(j + 1, std::integral_constant<int, 1>{});
+  }
+  if (j < ntiles) step(j, std::integral_constant<int, 0>{});
 
-    if (has_next) write_lds(buf ^ 1);
+  if constexpr (!SPLIT) {
+    pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);
+  } else {
+    const size_t prow0 = ((size_t)split * p.bh + bh) * (size_t)S;
+    pol.store_partial(make_rsrc(p.part_o + prow0 * HD, S * HD * 4), p.part_ml + prow0 * 2, qw, S,
+                      p.scale);
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Ping-pong skeleton (8 waves): group A = waves 0-3, group B = waves 4-7;
+// wave w and w+4 share a SIMD.  Every wave runs the phase sequence
+//   MFMA_0, SM_0, MFMA_1, SM_1, ..., SM_{n-1}, MFMA_n
+//   MFMA_k = qk(K_k) [k < n] + pv(V_{k-1}) [k >= 1]   (matrix pipe only)
+//   SM_k   = softmax(S_k)                              (VALU/transcendental)
+// Group A runs phase p in half-step p, group B in half-step p+1, and every
+// half-step ends at a workgroup barrier -- so on each SIMD one wave's MFMA
+// block always runs beside its partner's softmax (matrix || VALU), instead of
+// both waves hitting the same phase at once.
+// LDS: K and V double-buffered.  Tile k = (K_{k+1}, V_k) is loaded by group A
+// during MFMA_k and written during SM_k (half-steps 2k, 2k+1); group B loads
+// it one half-step earlier and writes it in half-step 2k.  K_{k+1}/V_k are
+// first read in half-step 2k+2 and their buffers were last read in half-step
+// 2k-1, so two buffers suffice.
+// ---------------------------------------------------------------------------
+template <class Pol, bool CAUSAL, bool SPLIT>
+__device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, int qb, int split,
+                                                   char* smem) {
+  constexpr int WAVES = 8;
+  constexpr int BN = Pol::BN;
+  constexpr int NT = WAVES * 64;
+  constexpr int BM = WAVES * 32;
+  constexpr int TILE_BYTES = BN * ROW_BYTES;
+  constexpr int NCH = (BN * 16) / NT;
+  static_assert((BN * 16) % NT == 0, "tile chunks must divide evenly");
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2;  // 0 = A, 1 = B (wave-uniform)
+  const int S = p.seq_len;
+
+  const size_t head_off = (size_t)bh * (size_t)S * HD;
+  const f16* Qh = p.q + head_off;
+  const f16* Kh = p.k + head_off;
+  const f16* Vh = p.v + head_off;
+
+  const int q0 = qb * BM;
+  const int qw = q0 + wave * 32;
+
+  int kv_lo = 0, kv_hi = CAUSAL ? min(q0 + BM, S) : S;
+  if constexpr (SPLIT) {
+    const int ntot = (kv_hi + BN - 1) / BN;
+    const int per = (ntot + p.num_splits - 1) / p.num_splits;
+    kv_lo = min(split * per, ntot) * BN;
+    kv_hi = min(kv_hi, min((split + 1) * per, ntot) * BN);
+  }
+  const int n = kv_hi > kv_lo ? (kv_hi - kv_lo + BN - 1) / BN : 0;
+
+  Pol pol;
+  pol.init(lane, p.c);
+  pol.load_q(make_rsrc(Qh, S * ROW_BYTES), qw);
+
+  char* kbuf0 = smem;
+  char* vbuf0 = smem + 2 * TILE_BYTES;
+  const int kr0 = pol.k_stage_row(wave), kc = pol.k_stage_ch();
+  const int vr0 = pol.v_stage_row(wave), vc = pol.v_stage_ch();
+  f16x8 kst[NCH], vst[NCH];
+  // tile k = (K_{k+1}, V_k); rows at/after kv_hi (or k >= n) read as 0
+  auto issue_tile = [&](int k) {
+    const int kb_row = kv_lo + (k + 1) * BN, vb_row = kv_lo + k * BN;
+    const auto rk = make_rsrc(Kh + (size_t)kb_row * HD, (kv_hi - kb_row) * ROW_BYTES);
+    const auto rv = make_rsrc(Vh + (size_t)vb_row * HD, (kv_hi - vb_row) * ROW_BYTES);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      kst[i] = buf_load16(rk, (kr0 + 4 * WAVES * i) * ROW_BYTES + kc * 16);
+      vst[i] = buf_load16(rv, (vr0 + 4 * WAVES * i) * ROW_BYTES + vc * 16);
+    }
+  };
+  auto write_tile = [&](int k) {
+    char* kb = kbuf0 + ((k + 1) & 1) * TILE_BYTES;
+    char* vb = vbuf0 + (k & 1) * TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      *reinterpret_cast<f16x8*>(kb + Pol::k_lds(kr0 + 4 * WAVES * i, kc)) = kst[i];
+      *reinterpret_cast<f16x8*>(vb + Pol::v_lds(vr0 + 4 * WAVES * i, vc)) = vst[i];
+    }
+  };
+
+  // prologue: K_0 by everyone; group B also issues tile 0 (written in half-step 0)
+  {
+    const auto rk = make_rsrc(Kh + (size_t)kv_lo * HD, (kv_hi - kv_lo) * ROW_BYTES);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      kst[i] = buf_load16(rk, (kr0 + 4 * WAVES * i) * ROW_BYTES + kc * 16);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      *reinterpret_cast<f16x8*>(kbuf0 + Pol::k_lds(kr0 + 4 * WAVES * i, kc)) = kst[i];
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // Q and K_0 retired before the loop (see attention_tile_loop)
+  if (grp == 1 && n > 0) issue_tile(0);
+  __syncthreads();
+
+  const float c = p.c;
+  auto active = [&](int k) { return !CAUSAL || (kv_lo + k * BN <= qw + 31); };
+  auto mfma_block = [&](int k) {
+    if (k >= 1 && active(k - 1)) pol.pv(vbuf0 + ((k - 1) & 1) * TILE_BYTES);
+    // keep the scheduler from hoisting QK's LDS reads into PV (register pressure)
+    __builtin_amdgcn_sched_barrier(0);
+    if (k < n && active(k)) pol.qk(kbuf0 + (k & 1) * TILE_BYTES);
+  };
+  auto softmax_block = [&](int k) {
+    if (k < n && active(k)) {
+      const int kv0 = kv_lo + k * BN;
+      const bool need_mask = (kv0 + BN > kv_hi) || (CAUSAL && kv0 + BN - 1 > qw);
+      pol.template softmax<CAUSAL>(kv0, kv_hi, qw, c, need_mask);
+    }
+  };
+
+  // Every wave runs the same loop [MFMA_k] barrier [SM_k] barrier; group B
+  // executes one extra barrier first (while A runs MFMA_0) and A one extra at
+  // the end, so B trails A by exactly one half-step with no group-specific
+  // code path.  Tile t = k + grp is loaded during MFMA_k and written during SM_k.
+  if (grp == 1) {
+    if (n > 0) write_tile(0);
     __syncthreads();
   }
+  for (int k = 0; k <= n; ++k) {
+    const int t = k + grp;
+    if (t < n) issue_tile(t);
+    mfma_block(k);
+    __syncthreads();
+    softmax_block(k);
+    if (t < n) write_tile(t);
+    __syncthreads();
+  }
+  if (grp == 0) __syncthreads();
 
-  // ---- epilogue: lane holds O^T[d = 32e + (i&3) + 8(i>>2) + 4h][q = qrow]
   if constexpr (!SPLIT) {
-    const float lt = sum_with_partner(l_run);
-    const float inv = lt > 0.f ? 1.0f / lt : 0.f;
-    if (qrow < S) {
-      f16* orow = p.o + head_off + (size_t)qrow * HD;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          f16x4 w;
-#pragma unroll
-          for (int x = 0; x < 4; ++x) w[x] = (f16)(acc[e][4 * g + x] * inv);
-          *reinterpret_cast<f16x4*>(orow + 32 * e + 8 * g + 4 * h) = w;
-        }
-      }
-    }
+    pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);
   } else {
-    const float lt = sum_with_partner(l_run);
-    if (qrow < S) {
-      const size_t prow = ((size_t)split * p.bh + bh) * (size_t)S + qrow;
-      float* po = p.part_o + prow * HD;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          float4 w = make_float4(acc[e][4 * g + 0], acc[e][4 * g + 1], acc[e][4 * g + 2],
-                                 acc[e][4 * g + 3]);
-          *reinterpret_cast<float4*>(po + 32 * e + 8 * g + 4 * h) = w;
-        }
-      if (h == 0) {
-        // m in the reference's units (scaled score = m_run*scale, ref m_i);
-        // an empty split writes (-inf, 0)
-        float2 ml = make_float2(lt > 0.f ? m_run * p.scale : -__builtin_inff(), lt);
-        *reinterpret_cast<float2*>(p.part_ml + prow * 2) = ml;
-      }
-    }
+    const size_t prow0 = ((size_t)split * p.bh + bh) * (size_t)S;
+    pol.store_partial(make_rsrc(p.part_o + prow0 * HD, S * HD * 4), p.part_ml + prow0 * 2, qw, S,
+                      p.scale);
   }
 }
 
