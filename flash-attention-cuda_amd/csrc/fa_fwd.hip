@@ -12,6 +12,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <mutex>
 
 #include "fa_fwd_kernel.hpp"
@@ -65,13 +66,14 @@ __device__ __forceinline__ void map_block(int id, int nblk, int nqb, int bh_coun
 }
 
 // SCHED: 0 = one-barrier-per-tile loop (any wave count), 1 = 8-wave ping-pong
+// (MFMA phase at s_setprio 1), 2 = ping-pong without the priority raise
 template <int WAVES, int BN, bool CAUSAL, bool SPLIT, bool USE_M16, int SCHED>
 __device__ __forceinline__ void run_tile_loop(const FwdParams& p, int bh, int qb, int split,
                                               char* smem) {
   using Pol = typename std::conditional<USE_M16, M16<BN>, M32<BN>>::type;
-  if constexpr (SCHED == 1) {
+  if constexpr (SCHED == 1 || SCHED == 2) {
     static_assert(WAVES == 8, "ping-pong needs two groups of four waves");
-    attention_pingpong<Pol, CAUSAL, SPLIT>(p, bh, qb, split, smem);
+    attention_pingpong<Pol, CAUSAL, SPLIT, SCHED == 1>(p, bh, qb, split, smem);
   } else {
     attention_tile_loop<Pol, WAVES, CAUSAL, SPLIT>(p, bh, qb, split, smem);
   }
@@ -80,9 +82,85 @@ __device__ __forceinline__ void run_tile_loop(const FwdParams& p, int bh, int qb
 template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED>
 __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+#ifdef FA_STAMPS
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
   int qb, bh;
   map_block(blockIdx.x, gridDim.x, p.nqb, p.bh, p.band, CAUSAL, qb, bh);
   run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED>(p, bh, qb, 0, smem);
+#ifdef FA_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < FA_MAX_TIMELINE) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_fa_timeline[blockIdx.x][0] = t_start;
+    g_fa_timeline[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+    g_fa_timeline[blockIdx.x][2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+  }
+#endif
+}
+
+// Persistent variant: gridDim = 8 x C workgroups, one per CU.
+// Workgroups b, b+8, ... share an XCD; XCD x owns heads x, x+8, ... and walks
+// its item list (causal: rank bands of `band` query blocks of one head,
+// heaviest band first; non-causal: head-major) in rounds of C items, the
+// C workgroups taking a round in snake order (forward on even rounds,
+// reversed on odd ones).  Within a band the item costs fall linearly, so the
+// snake makes every CU's cost equal over each pair of rounds -- LPT balance
+// by construction, with no atomics or per-launch state -- while the items of
+// one round (one or two heads' query blocks) co-run on the XCD and share K/V
+// through its L2.
+__device__ __forceinline__ void xcd_item(int j, int hx, int nqb, int band, bool causal, int& lh,
+                                         int& rank) {
+  if (!causal) {
+    lh = j / nqb;
+    rank = j - lh * nqb;
+    return;
+  }
+  const int r = min(nqb, max(band, 1));
+  const int full = nqb / r, rl = nqb - full * r;
+  if (j < full * hx * r) {
+    const int bnd = j / (hx * r), k = j - bnd * hx * r;
+    lh = k / r;
+    rank = bnd * r + (k - lh * r);
+  } else {
+    const int k = j - full * hx * r;
+    lh = k / rl;
+    rank = full * r + (k - lh * rl);
+  }
+}
+
+template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED>
+__global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(FwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int x = blockIdx.x & 7, lcu = blockIdx.x >> 3, C = gridDim.x >> 3;
+  const int hx = (p.bh - x + 7) >> 3;  // heads h < bh with h % 8 == x
+  const int L = hx * p.nqb;
+  for (int r = 0; r * C < L; ++r) {
+    const int pos = r * C + ((r & 1) ? (C - 1 - lcu) : lcu);
+    if (pos < L) {
+      int lh, rank;
+      xcd_item(pos, hx, p.nqb, p.band, CAUSAL, lh, rank);
+      const int bh = x + 8 * lh;
+      const int qb = CAUSAL ? p.nqb - 1 - rank : rank;
+#ifdef FA_STAMPS
+      const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+      run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED>(p, bh, qb, 0, smem);
+#ifdef FA_STAMPS
+      const int rec = bh * p.nqb + qb;
+      if (threadIdx.x == 0 && rec < FA_MAX_TIMELINE) {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_fa_timeline[rec][0] = t_start;
+        g_fa_timeline[rec][1] = __builtin_amdgcn_s_memrealtime();
+        g_fa_timeline[rec][2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+      }
+#endif
+    }
+    __syncthreads();  // LDS images are reused by the next item
+  }
 }
 
 // Split-KV: workgroup id -> (split, item); items ordered as map_block.
@@ -135,20 +213,24 @@ struct Config {
   fa_config_info_t info;
   int mfma;   // 32 = v_mfma_f32_32x32x16_f16 loop, 16 = v_mfma_f32_16x16x32_f16 loop
   int sched;  // 0 = one barrier per tile, 1 = 8-wave ping-pong
+  int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent
   kernel_fn fn;
 };
 
 template <int W, int BN_, int C, int SPL, int M, int SCHED>
 constexpr kernel_fn pick_kernel() {
-  if constexpr (SPL)
+  if constexpr (SPL == 1)
     return fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
+  else if constexpr (SPL == 2)
+    return fa_fwd_f16_persistent_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
   else
     return fa_fwd_f16_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
 }
 
-#define FA_CFG(ID, W, BN_, C, SPL, M, SCHED, NAME)                                     \
-  {{ID, 32 * (W), BN_, W, C, SPL, 4 * (BN_) * ROW_BYTES, NAME}, M, SCHED, \
-   pick_kernel<W, BN_, C, SPL, M, SCHED>()}
+// KIND: 0 = one workgroup per (head, query block), 1 = split-KV, 2 = persistent
+#define FA_CFG(ID, W, BN_, C, KIND, M, SCHED, NAME)                                       \
+  {{ID, 32 * (W), BN_, W, C, (KIND) == 1, 4 * (BN_) * ROW_BYTES, NAME}, M, SCHED, KIND, \
+   pick_kernel<W, BN_, C, KIND, M, SCHED>()}
 
 static const Config kConfigs[] = {
     FA_CFG(0, 4, 64, 0, 0, 32, 0, "bm128_bn64_w4_m32_noncausal"),
@@ -165,6 +247,8 @@ static const Config kConfigs[] = {
     FA_CFG(11, 8, 64, 1, 0, 32, 1, "bm256_bn64_w8_m32_pingpong_causal"),
     FA_CFG(12, 4, 64, 0, 1, 16, 0, "bm128_bn64_w4_m16_noncausal_splitkv"),
     FA_CFG(13, 4, 64, 1, 1, 16, 0, "bm128_bn64_w4_m16_causal_splitkv"),
+    FA_CFG(14, 8, 64, 0, 2, 16, 1, "bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
+    FA_CFG(15, 8, 64, 1, 2, 16, 1, "bm256_bn64_w8_m16_pingpong_persistent_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -182,13 +266,28 @@ static int prepare(int id) {
 }
 
 // causal rank-band width (query blocks of one head kept together on an XCD);
-// FA_CAUSAL_BAND overrides it for tuning (<= 1 = plain heaviest-first order)
+// FA_CAUSAL_BAND overrides the automatic choice for tuning (1 = plain
+// heaviest-first order)
 static int causal_band() {
   static int band = [] {
     const char* e = getenv("FA_CAUSAL_BAND");
-    return e ? atoi(e) : 16;
+    return e ? atoi(e) : 0;  // 0 = automatic
   }();
   return band;
+}
+
+// CUs of the current device (cached per device id)
+static int num_cus() {
+  static int cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
 }
 
 static int check_args(const void* q, const void* k, const void* v, const void* o, int batch,
@@ -220,9 +319,17 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   p.num_splits = num_splits;
   p.scale = 1.0f / sqrtf((float)HD);          // ref :612
   p.c = p.scale * 1.4426950408889634f;        // LOG2E, ref :239
-  p.band = causal_band();
-  const long long blocks = (long long)p.nqb * bh * num_splits;
+  // few heads per XCD: plain heaviest-first balances better; many: keep the
+  // query blocks of a head together for L2 reuse (profiles/r01_band_ab.txt)
+  p.band = causal_band() > 0 ? causal_band() : (bh <= 64 ? 1 : 16);
+  long long blocks = (long long)p.nqb * bh * num_splits;
   if (blocks > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
+  if (cfg.kind == 2) {
+    // one workgroup per CU, 8 per XCD group; never more than the items per XCD
+    const long long per_xcd = (long long)((bh + 7) / 8) * p.nqb;
+    const long long c = std::min<long long>(std::max(1, num_cus() / 8), per_xcd);
+    blocks = 8 * c;
+  }
   hipLaunchKernelGGL(cfg.fn, dim3((unsigned)blocks), dim3(cfg.info.waves * 64),
                      cfg.info.lds_bytes, stream, p);
   return hipGetLastError() == hipSuccess ? FA_OK : FA_ERR_LAUNCH;
@@ -231,7 +338,7 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
 static int cfg_for(int waves, int bn, int causal, int mfma, int sched) {
   for (int i = 0; i < kNumConfigs; ++i)
     if (kConfigs[i].info.waves == waves && kConfigs[i].info.block_n == bn &&
-        kConfigs[i].info.causal == causal && !kConfigs[i].info.split_kv &&
+        kConfigs[i].info.causal == causal && kConfigs[i].kind == 0 &&
         kConfigs[i].mfma == mfma && kConfigs[i].sched == sched)
       return i;
   return -1;
@@ -372,3 +479,21 @@ extern "C" const char* fa_status_string(int status) {
 }
 
 extern "C" const char* fa_version(void) { return "fa_mi355x 0.1 (gfx950)"; }
+
+#ifdef FA_STAMPS
+extern "C" int fa_debug_timeline(unsigned long long* out, int n) {
+  if (n > FA_MAX_TIMELINE) n = FA_MAX_TIMELINE;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(fa::g_fa_timeline), (size_t)n * 24) == hipSuccess
+             ? FA_OK
+             : FA_ERR_HIP;
+}
+extern "C" int fa_debug_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fa::g_fa_stamps), sizeof(fa::g_fa_stamps)) != hipSuccess)
+    return FA_ERR_HIP;
+  if (reset) {
+    static const unsigned long long z[8][5] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(fa::g_fa_stamps), z, sizeof(z)) != hipSuccess) return FA_ERR_HIP;
+  }
+  return FA_OK;
+}
+#endif

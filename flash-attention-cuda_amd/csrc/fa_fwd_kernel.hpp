@@ -125,6 +125,16 @@ __device__ __forceinline__ f16x4 lds_read_tr(const char* base, int off) {
 
 __device__ __forceinline__ float ninf() { return -__builtin_inff(); }
 
+#ifdef FA_STAMPS
+// diagnostic build only (lib/libfa_mi355x_stamps.so): per-wave cycles spent in
+// [MFMA block, barrier after it, softmax block, barrier after it, LDS tile write], summed over
+// the first 64 workgroups.  Never part of the product library.
+__device__ unsigned long long g_fa_stamps[8][5];
+// per-workgroup timeline: {start, end (s_memrealtime, 100 MHz), hw_id | xcc_id << 32}
+constexpr int FA_MAX_TIMELINE = 65536;
+__device__ unsigned long long g_fa_timeline[FA_MAX_TIMELINE][3];
+#endif
+
 // ---------------------------------------------------------------------------
 // Policies.  Each holds one wave's state (Q fragments, O accumulator, running
 // max/sum, the current S^T tile and its fp16 P) and splits a key tile into
@@ -149,10 +159,15 @@ struct M32 {
   f32x16 acc[4];
   f32x16 s[NSB];
   f16x8 pf[BN / 16];
-  float m_run, l_run;
+  f32x16 negm;    // C operand of the QK^T chains: -m_ref broadcast
+  f32x16 lacc;    // running row sums (ones . P in the PV chain); every register = l(q)
+  float m_ref;    // reference max, log2 units (x = s*c - m_ref)
+  bool have_ref;  // wave-uniform: a tile has set m_ref
+  float c;
 
-  __device__ __forceinline__ void init(int lane_, float /*c*/) {
+  __device__ __forceinline__ void init(int lane_, float c_) {
     lane = lane_;
+    c = c_;
     r = lane & 31;
     h = lane >> 5;
     // K row read (A of S^T): row 32cb+r, chunk 2t+h -> 8192cb + 512(t>>1) + kaddr[t&1]
@@ -166,13 +181,20 @@ struct M32 {
     vaddr1 = 2048 + base + 16 * ((2 * (G & 1) + (pp >> 1)) ^ (2 + h));
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc[e] = f32x16{};
-    m_run = ninf();
-    l_run = 0.f;
+    negm = f32x16{};
+    lacc = f32x16{};
+    m_ref = 0.f;
+    have_ref = false;
   }
-  // Q (B operand of S^T): lane holds Q[qw + r][16t + 8h .. +7]
+  // Q (B operand of S^T): lane holds c * Q[qw + r][16t + 8h .. +7]  (fp16)
   __device__ __forceinline__ void load_q(__amdgpu_buffer_rsrc_t rq, int qw) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) qf[t] = buf_load16(rq, (qw + r) * ROW_BYTES + (2 * t + h) * 16);
+    for (int t = 0; t < 8; ++t) {
+      f16x8 x = buf_load16(rq, (qw + r) * ROW_BYTES + (2 * t + h) * 16);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = (f16)((float)x[j] * c);
+      qf[t] = x;
+    }
   }
   // staging: 8 consecutive lanes = two rows of opposite parity x 4 chunks
   // (conflict-free ds_write_b128 into image A)
@@ -187,19 +209,17 @@ struct M32 {
 
   __device__ __forceinline__ void qk(const char* kb) {
 #pragma unroll
-    for (int cb = 0; cb < NSB; ++cb) s[cb] = f32x16{};
-#pragma unroll
     for (int t = 0; t < 8; ++t) {
       const int ka = ((t & 1) ? kaddr1 : kaddr0) + 512 * (t >> 1);
 #pragma unroll
       for (int cb = 0; cb < NSB; ++cb) {
         const f16x8 kf = *reinterpret_cast<const f16x8*>(kb + ka + 8192 * cb);
-        s[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[t], s[cb], 0, 0, 0);
+        s[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[t], t == 0 ? negm : s[cb], 0, 0, 0);
       }
     }
   }
   template <bool CAUSAL>
-  __device__ __forceinline__ void softmax(int kv0, int kv_hi, int qw, float c, bool need_mask) {
+  __device__ __forceinline__ void softmax(int kv0, int kv_hi, int qw, float /*c*/, bool need_mask) {
     if (need_mask) {
       const int qrow = qw + r;
 #pragma unroll
@@ -211,34 +231,38 @@ struct M32 {
           s[cb][i] = ok ? s[cb][i] : ninf();
         }
     }
+    // row max relative to m_ref; move m_ref only when it grew by > RESCALE_LOG2
     float mx = s[0][0];
 #pragma unroll
     for (int cb = 0; cb < NSB; ++cb)
 #pragma unroll
       for (int i = (cb == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, s[cb][i]);
     mx = max_xor32(mx);
-    const float m_new = fmaxf(m_run, mx);
-    if (__any((m_new - m_run) * c > RESCALE_LOG2)) {
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+    if (__any(!have_ref || mx > RESCALE_LOG2)) {
+      // first tile: centre on the max; later: only ever move m_ref up.
+      // A row with every key masked (mx = -inf) keeps m_ref.
+      float sh = have_ref ? fmaxf(mx, 0.f) : mx;
+      sh = sh == ninf() ? 0.f : sh;
+      if (have_ref) {
+        const float alpha = __builtin_amdgcn_exp2f(-sh);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[e] *= alpha;
-      l_run *= alpha;
-      m_run = m_new;
+        for (int e = 0; e < 4; ++e) acc[e] *= alpha;
+        lacc *= alpha;
+      }
+#pragma unroll
+      for (int cb = 0; cb < NSB; ++cb) s[cb] -= sh;
+      m_ref += sh;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) negm[i] = -m_ref;
+      have_ref = true;
     }
-    // m_run stays -inf only for a row with no visible key yet: keep P = 0, not NaN
-    const float mc = m_run == ninf() ? 0.f : m_run * c;
-    float lsum = 0.f;
 #pragma unroll
     for (int cb = 0; cb < NSB; ++cb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[cb][i], c, -mc));
-        lsum += pv;
-        pf[2 * cb + (i >> 3)][i & 7] = (f16)pv;
-      }
-    l_run += lsum;
+      for (int i = 0; i < 16; ++i) pf[2 * cb + (i >> 3)][i & 7] = (f16)__builtin_amdgcn_exp2f(s[cb][i]);
   }
   __device__ __forceinline__ void pv(const char* vb) {
+    const f16x8 ones = {(f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1};
 #pragma unroll
     for (int u = 0; u < BN / 16; ++u) {
       const int cb = u >> 1, sb = u & 1;
@@ -250,19 +274,25 @@ struct M32 {
         const f16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
         acc[e] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[u], acc[e], 0, 0, 0);
       }
+      lacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ones, pf[u], lacc, 0, 0, 0);
     }
   }
   template <bool CAUSAL>
   __device__ __forceinline__ void tile(const char* kb, const char* vb, int kv0, int kv_hi, int qw,
-                                       float c, bool need_mask) {
+                                       float c_, bool need_mask) {
     qk(kb);
-    softmax<CAUSAL>(kv0, kv_hi, qw, c, need_mask);
+    softmax<CAUSAL>(kv0, kv_hi, qw, c_, need_mask);
     pv(vb);
+  }
+  __device__ __forceinline__ void mfma_block(const char* kb, const char* vb, bool do_pv, bool do_qk) {
+    if (do_pv) pv(vb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (do_qk) qk(kb);
   }
 
   // lane holds O^T[d = 32e + (i&3) + 8(i>>2) + 4h][q = qw + r]
   __device__ __forceinline__ void store_o(__amdgpu_buffer_rsrc_t ro, int qw) {
-    const float lt = sum_xor32(l_run);
+    const float lt = lacc[0];
     const float inv = lt > 0.f ? 1.0f / lt : 0.f;
     const int rowb = (qw + r) * ROW_BYTES;
 #pragma unroll
@@ -275,9 +305,10 @@ struct M32 {
         buf_store8(ro, rowb + 2 * (32 * e + 8 * g + 4 * h), w);
       }
   }
+  // m in the reference's units (scaled score, natural log): m_ref * ln 2
   __device__ __forceinline__ void store_partial(__amdgpu_buffer_rsrc_t rpo, float* pml, int qw,
-                                                int S, float scale) {
-    const float lt = sum_xor32(l_run);
+                                                int S, float /*scale*/) {
+    const float lt = lacc[0];
     const int rowb = (qw + r) * HD * 4;
 #pragma unroll
     for (int e = 0; e < 4; ++e)
@@ -287,7 +318,7 @@ struct M32 {
                      f32x4{acc[e][4 * g], acc[e][4 * g + 1], acc[e][4 * g + 2], acc[e][4 * g + 3]});
     if (h == 0 && qw + r < S)
       *reinterpret_cast<float2*>(pml + (size_t)(qw + r) * 2) =
-          make_float2(lt > 0.f ? m_run * scale : ninf(), lt);
+          make_float2(lt > 0.f ? m_ref * 0.6931471805599453f : ninf(), lt);
   }
 };
 
@@ -324,7 +355,7 @@ struct M16 {
   f16x8 pf[2][NU];
   f32x4 negm[2];     // C operand of the QK^T chains: -m_ref broadcast
   float m_ref[2];    // reference max, log2 units (x = s*c - m_ref)
-  float l_run[2];
+  f32x4 lacc[2];     // running row sums l (ones . P on the matrix pipe, in the PV chain)
   bool have_ref;     // wave-uniform: a tile has set m_ref
   float c;
 
@@ -348,7 +379,7 @@ struct M16 {
       for (int e = 0; e < 8; ++e) acc[b][e] = f32x4{};
       negm[b] = f32x4{};
       m_ref[b] = 0.f;
-      l_run[b] = 0.f;
+      lacc[b] = f32x4{};
     }
     have_ref = false;
   }
@@ -380,29 +411,26 @@ struct M16 {
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int cb = 0; cb < NKB; ++cb) {
+#ifdef FA_DIAG_NO_LDS  // diagnostic timing build only: operands from registers
+        const f16x8 kf = qf[cb & 1][(t + cb) & 3];
+#else
         const f16x8 kf = *reinterpret_cast<const f16x8*>(kb + kaddr[t] + 4096 * cb);
+#endif
 #pragma unroll
         for (int b = 0; b < 2; ++b)
           s[b][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[b][t], t == 0 ? negm[b] : s[b][cb],
                                                             0, 0, 0);
       }
   }
-  // P = exp2(x) -> fp16 (B operand layout of the PV product), and the tile's
-  // row sums lt[b] (every register of lt[b] holds the sum for q = lane&15)
-  __device__ __forceinline__ void exp_and_sum(f32x4 (&lt)[2]) {
-    const f16x8 ones = {(f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1};
+  // P = exp2(x) -> fp16, already in the B-operand layout of the PV product
+  __device__ __forceinline__ void exp_p() {
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int cb = 0; cb < NKB; ++cb)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           pf[b][cb >> 1][4 * (cb & 1) + i] = (f16)__builtin_amdgcn_exp2f(s[b][cb][i]);
-      lt[b] = f32x4{};
-#pragma unroll
-      for (int u = 0; u < NU; ++u)
-        lt[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, pf[b][u], lt[b], 0, 0, 0);
-    }
   }
   template <bool CAUSAL>
   __device__ __forceinline__ void softmax(int kv0, int kv_hi, int qw, float /*c*/, bool need_mask) {
@@ -445,7 +473,7 @@ struct M16 {
           const float alpha = __builtin_amdgcn_exp2f(-sh);
 #pragma unroll
           for (int e = 0; e < 8; ++e) acc[b][e] *= alpha;
-          l_run[b] *= alpha;
+          lacc[b] *= alpha;
         }
 #pragma unroll
         for (int cb = 0; cb < NKB; ++cb) s[b][cb] -= sh;
@@ -454,24 +482,38 @@ struct M16 {
       }
       have_ref = true;
     }
-    f32x4 lt[2];
-    exp_and_sum(lt);
-    l_run[0] += lt[0][0];
-    l_run[1] += lt[1][0];
+    exp_p();
   }
   __device__ __forceinline__ void pv(const char* vb) {
+    const f16x8 ones = {(f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1};
 #pragma unroll
-    for (int u = 0; u < NU; ++u)
+    for (int u = 0; u < NU; ++u) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
+#ifdef FA_DIAG_NO_LDS
+        const f16x8 vf = qf[e & 1][(u + e) & 3];
+#else
         const int base = 8192 * u + 512 * (e >> 1) + vaddr[e & 1];
         const f16x4 lo = lds_read_tr(vb, base);
         const f16x4 hi = lds_read_tr(vb, base + 4096);
         const f16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#endif
 #pragma unroll
         for (int b = 0; b < 2; ++b)
           acc[b][e] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[b][u], acc[b][e], 0, 0, 0);
       }
+      // row sums of the same fp16 P: every register of lacc[b] = l for q = lane&15
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        lacc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, pf[b][u], lacc[b], 0, 0, 0);
+    }
+  }
+  // the ping-pong MFMA block: PV(V_{k-1}) then QK^T(K_k); the barrier keeps the
+  // scheduler from hoisting QK's LDS reads into PV (register pressure)
+  __device__ __forceinline__ void mfma_block(const char* kb, const char* vb, bool do_pv, bool do_qk) {
+    if (do_pv) pv(vb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (do_qk) qk(kb);
   }
   template <bool CAUSAL>
   __device__ __forceinline__ void tile(const char* kb, const char* vb, int kv0, int kv_hi, int qw,
@@ -484,7 +526,7 @@ struct M16 {
   __device__ __forceinline__ void store_o(__amdgpu_buffer_rsrc_t ro, int qw) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
-      const float lt = l_run[b];  // already the full row sum (MFMA over all keys)
+      const float lt = lacc[b][0];  // already the full row sum (MFMA over all keys)
       const float inv = lt > 0.f ? 1.0f / lt : 0.f;
       const int rowb = (qw + 16 * b + r16) * ROW_BYTES;
 #pragma unroll
@@ -501,7 +543,7 @@ struct M16 {
                                                 int S, float /*scale*/) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
-      const float lt = l_run[b];
+      const float lt = lacc[b][0];
       const int q = qw + 16 * b + r16;
 #pragma unroll
       for (int e = 0; e < 8; ++e) buf_store16f(rpo, q * HD * 4 + 4 * (16 * e + 4 * g), acc[b][e]);
@@ -637,7 +679,7 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
 // first read in half-step 2k+2 and their buffers were last read in half-step
 // 2k-1, so two buffers suffice.
 // ---------------------------------------------------------------------------
-template <class Pol, bool CAUSAL, bool SPLIT>
+template <class Pol, bool CAUSAL, bool SPLIT, bool PRIO = true>
 __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, int qb, int split,
                                                    char* smem) {
   constexpr int WAVES = 8;
@@ -718,10 +760,12 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   const float c = p.c;
   auto active = [&](int k) { return !CAUSAL || (kv_lo + k * BN <= qw + 31); };
   auto mfma_block = [&](int k) {
-    if (k >= 1 && active(k - 1)) pol.pv(vbuf0 + ((k - 1) & 1) * TILE_BYTES);
-    // keep the scheduler from hoisting QK's LDS reads into PV (register pressure)
-    __builtin_amdgcn_sched_barrier(0);
-    if (k < n && active(k)) pol.qk(kbuf0 + (k & 1) * TILE_BYTES);
+    // the MFMA-phase wave wins VALU/MFMA issue arbitration against its SIMD
+    // partner (which is in its softmax phase), so its matrix stream stays dense
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+    pol.mfma_block(kbuf0 + (k & 1) * TILE_BYTES, vbuf0 + ((k - 1) & 1) * TILE_BYTES,
+                   k >= 1 && active(k - 1), k < n && active(k));
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   };
   auto softmax_block = [&](int k) {
     if (k < n && active(k)) {
@@ -739,16 +783,50 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     if (n > 0) write_tile(0);
     __syncthreads();
   }
+#ifdef FA_STAMPS
+  unsigned long long st_acc[5] = {0, 0, 0, 0, 0}, st0, st1, st2, st3, st4;
+#define FA_STAMP(v)                                                                   \
+  do {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");         \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+  } while (0)
+#else
+#define FA_STAMP(v) \
+  do {              \
+  } while (0)
+#endif
   for (int k = 0; k <= n; ++k) {
     const int t = k + grp;
+    FA_STAMP(st0);
     if (t < n) issue_tile(t);
     mfma_block(k);
+    FA_STAMP(st1);
     __syncthreads();
+    FA_STAMP(st2);
     softmax_block(k);
+#ifdef FA_STAMPS
+    unsigned long long st25;
+    FA_STAMP(st25);
+#endif
     if (t < n) write_tile(t);
+    FA_STAMP(st3);
     __syncthreads();
+    FA_STAMP(st4);
+#ifdef FA_STAMPS
+    st_acc[0] += st1 - st0;
+    st_acc[1] += st2 - st1;
+    st_acc[2] += st25 - st2;
+    st_acc[3] += st4 - st3;
+    st_acc[4] += st3 - st25;
+#endif
   }
   if (grp == 0) __syncthreads();
+#ifdef FA_STAMPS
+  if (lane == 0 && blockIdx.x < 64)
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
+#endif
+#undef FA_STAMP
 
   if constexpr (!SPLIT) {
     pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);

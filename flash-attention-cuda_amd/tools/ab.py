@@ -1,0 +1,52 @@
+"""Interleaved A/B timing of tile configs in ONE process (guide §5.4 rule 24).
+usage: python tools/ab.py --configs 8,10 --seq 8192 [--causal] [--batch B] [--heads H]
+       [--rounds 7] [--iters 30]
+Prints per-config median / min TFLOPS over rounds (random uniform[-0.5,0.5] fp16)."""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import fa_mi355x as fa  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--configs", required=True)
+ap.add_argument("--seq", type=int, default=8192)
+ap.add_argument("--heads", type=int, default=32)
+ap.add_argument("--batch", type=int, default=1)
+ap.add_argument("--causal", action="store_true")
+ap.add_argument("--rounds", type=int, default=7)
+ap.add_argument("--iters", type=int, default=30)
+ap.add_argument("--env", default="", help="label only")
+a = ap.parse_args()
+g = torch.Generator(device="cuda")
+g.manual_seed(3)
+shape = (a.batch, a.heads, a.seq, 128)
+q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5, generator=g)
+           for _ in range(3))
+o = torch.empty_like(q)
+cids = [int(x) for x in a.configs.split(",")]
+flops = fa.attention_flops(a.batch, a.heads, a.seq, 128, a.causal)
+res = {c: [] for c in cids}
+for c in cids:  # warm
+    for _ in range(5):
+        fa.flash_attention_fwd(q, k, v, a.causal, out=o, config=c)
+torch.cuda.synchronize()
+for _ in range(a.rounds):
+    for c in cids:
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        for _ in range(a.iters):
+            fa.flash_attention_fwd(q, k, v, a.causal, out=o, config=c)
+        en.record()
+        en.synchronize()
+        res[c].append(flops / (st.elapsed_time(en) / a.iters / 1e3) / 1e12)
+names = {c.id: c.name for c in fa.configs()}
+for c in cids:
+    print(json.dumps({"config": names[c], "seq": a.seq, "batch": a.batch, "causal": a.causal,
+                      "median_tflops": round(statistics.median(res[c]), 1),
+                      "min_tflops": round(min(res[c]), 1), "max_tflops": round(max(res[c]), 1)}))

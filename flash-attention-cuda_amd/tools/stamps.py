@@ -1,0 +1,39 @@
+"""Phase-stamp diagnostic (loads lib/libfa_mi355x_stamps.so, NOT the product lib).
+usage: python tools/stamps.py --config 8 --seq 8192 [--causal] [--batch B]
+Prints per-wave mean cycles per loop iteration in: MFMA block, barrier-1, softmax block, barrier-2."""
+import argparse
+import ctypes
+import os
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+import fa_mi355x as fa  # noqa: E402
+
+fa.LIB_PATH = os.path.join(HERE, "lib", os.environ.get("FA_STAMPS_LIB", "libfa_mi355x_stamps.so"))
+import torch  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", type=int, required=True)
+ap.add_argument("--seq", type=int, default=8192)
+ap.add_argument("--batch", type=int, default=1)
+ap.add_argument("--heads", type=int, default=32)
+ap.add_argument("--causal", action="store_true")
+a = ap.parse_args()
+lib = fa.load_library()
+lib.fa_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+buf = (ctypes.c_ulonglong * 40)()
+shape = (a.batch, a.heads, a.seq, 128)
+q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5) for _ in range(3))
+fa.flash_attention_fwd(q, k, v, a.causal, config=a.config)
+torch.cuda.synchronize()
+lib.fa_debug_stamps(buf, 1)
+fa.flash_attention_fwd(q, k, v, a.causal, config=a.config)
+torch.cuda.synchronize()
+lib.fa_debug_stamps(buf, 1)
+tiles = (a.seq + 63) // 64
+iters = 64 * (tiles + 1)  # 64 workgroups x (n+1) loop iterations (non-causal)
+print("wave  mfma_blk  bar1  softmax  bar2  lds_write  (cycles per iteration, first 64 workgroups)")
+for w in range(8):
+    vals = [buf[w * 5 + i] / iters for i in range(5)]
+    print(w, " ".join(f"{x:9.0f}" for x in vals), f" total {sum(vals):.0f}")

@@ -1,0 +1,52 @@
+"""Workgroup timeline diagnostic (stamps build): per-CU busy fraction, tail, order.
+usage: python tools/timeline.py --config 9 --seq 8192 --causal [--batch B]"""
+import argparse
+import collections
+import ctypes
+import os
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+import fa_mi355x as fa  # noqa: E402
+
+fa.LIB_PATH = os.path.join(HERE, "lib", "libfa_mi355x_stamps.so")
+import torch  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", type=int, required=True)
+ap.add_argument("--seq", type=int, default=8192)
+ap.add_argument("--batch", type=int, default=1)
+ap.add_argument("--heads", type=int, default=32)
+ap.add_argument("--causal", action="store_true")
+a = ap.parse_args()
+lib = fa.load_library()
+lib.fa_debug_timeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
+cfg = fa.configs()[a.config]
+nblk = a.batch * a.heads * ((a.seq + cfg.block_m - 1) // cfg.block_m)  # records: one per item
+shape = (a.batch, a.heads, a.seq, 128)
+q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5) for _ in range(3))
+for _ in range(3):
+    fa.flash_attention_fwd(q, k, v, a.causal, config=a.config)
+torch.cuda.synchronize()
+n = min(nblk, 65536)
+buf = (ctypes.c_ulonglong * (3 * n))()
+lib.fa_debug_timeline(buf, n)
+rows = [(buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]) for i in range(n)]
+t0 = min(r[0] for r in rows)
+t1 = max(r[1] for r in rows)
+span = (t1 - t0) / 100.0  # us
+cu = collections.defaultdict(float)
+for s_, e_, hw in rows:
+    h = hw & 0xFFFFFFFF
+    key = (hw >> 32, (h >> 13) & 7, (h >> 12) & 1, (h >> 8) & 15)  # xcc, se, sh, cu
+    cu[key] += (e_ - s_) / 100.0
+busy = sorted(cu.values())
+durs = sorted((e_ - s_) / 100.0 for s_, e_, _ in rows)
+ends = sorted((e_ - t0) / 100.0 for _, e_, _ in rows)
+print(f"{cfg.name} seq={a.seq} batch={a.batch}: {n} workgroups on {len(cu)} CUs, span {span:.1f} us")
+print(f"  CU busy: mean {sum(busy)/len(busy):.1f} us ({100*sum(busy)/len(busy)/span:.1f}%), "
+      f"min {busy[0]:.1f}, max {busy[-1]:.1f}")
+print(f"  workgroup duration: min {durs[0]:.2f} med {durs[len(durs)//2]:.2f} max {durs[-1]:.2f} us")
+print(f"  last 1% of workgroups end after {ends[int(0.99*len(ends))]:.1f} us; "
+      f"first end {ends[0]:.1f} us")
