@@ -22,6 +22,8 @@ ap.add_argument("--causal", action="store_true")
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--iters", type=int, default=30)
 ap.add_argument("--env", default="", help="label only")
+ap.add_argument("--libs", default="", help="comma list of library variants: '' = libfa_mi355x.so, "
+                "X = libfa_mi355x_X.so; every config is timed against every variant")
 a = ap.parse_args()
 g = torch.Generator(device="cuda")
 g.manual_seed(3)
@@ -29,24 +31,32 @@ shape = (a.batch, a.heads, a.seq, 128)
 q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5, generator=g)
            for _ in range(3))
 o = torch.empty_like(q)
-cids = [int(x) for x in a.configs.split(",")]
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+libs = {}
+for var in a.libs.split(","):
+    fa._lib = None
+    fa.LIB_PATH = os.path.join(HERE, "lib", "libfa_mi355x%s.so" % ("_" + var if var else ""))
+    libs[var] = fa.load_library()
+cids = [(var, int(x)) for x in a.configs.split(",") for var in libs]
 flops = fa.attention_flops(a.batch, a.heads, a.seq, 128, a.causal)
 res = {c: [] for c in cids}
 for c in cids:  # warm
+    fa._lib = libs[c[0]]
     for _ in range(5):
-        fa.flash_attention_fwd(q, k, v, a.causal, out=o, config=c)
+        fa.flash_attention_fwd(q, k, v, a.causal, out=o, config=c[1])
 torch.cuda.synchronize()
 for _ in range(a.rounds):
     for c in cids:
+        fa._lib = libs[c[0]]
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st.record()
         for _ in range(a.iters):
-            fa.flash_attention_fwd(q, k, v, a.causal, out=o, config=c)
+            fa.flash_attention_fwd(q, k, v, a.causal, out=o, config=c[1])
         en.record()
         en.synchronize()
         res[c].append(flops / (st.elapsed_time(en) / a.iters / 1e3) / 1e12)
 names = {c.id: c.name for c in fa.configs()}
 for c in cids:
-    print(json.dumps({"config": names[c], "seq": a.seq, "batch": a.batch, "causal": a.causal,
+    print(json.dumps({"config": names[c[1]], "lib": c[0] or "base", "seq": a.seq, "batch": a.batch, "causal": a.causal,
                       "median_tflops": round(statistics.median(res[c]), 1),
                       "min_tflops": round(min(res[c]), 1), "max_tflops": round(max(res[c]), 1)}))
