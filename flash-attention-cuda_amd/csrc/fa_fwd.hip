@@ -84,6 +84,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_kernel(FwdParams p) 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 #ifdef FA_STAMPS
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long c_start = __builtin_amdgcn_s_memtime();
 #endif
   int qb, bh;
   map_block(blockIdx.x, gridDim.x, p.nqb, p.bh, p.band, CAUSAL, qb, bh);
@@ -95,7 +96,9 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_kernel(FwdParams p) 
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     g_fa_timeline[blockIdx.x][0] = t_start;
     g_fa_timeline[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
-    g_fa_timeline[blockIdx.x][2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+    g_fa_timeline[blockIdx.x][3] = __builtin_amdgcn_s_memtime() - c_start;
+    g_fa_timeline[blockIdx.x][2] =
+        (unsigned long long)hw | ((unsigned long long)xcc << 32) | ((unsigned long long)qb << 40);
   }
 #endif
 }
@@ -145,6 +148,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(Fw
       const int qb = CAUSAL ? p.nqb - 1 - rank : rank;
 #ifdef FA_STAMPS
       const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+      const unsigned long long c_start = __builtin_amdgcn_s_memtime();
 #endif
       run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED>(p, bh, qb, 0, smem);
 #ifdef FA_STAMPS
@@ -155,12 +159,37 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(Fw
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         g_fa_timeline[rec][0] = t_start;
         g_fa_timeline[rec][1] = __builtin_amdgcn_s_memrealtime();
-        g_fa_timeline[rec][2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+        g_fa_timeline[rec][3] = __builtin_amdgcn_s_memtime() - c_start;
+        g_fa_timeline[rec][2] =
+            (unsigned long long)hw | ((unsigned long long)xcc << 32) | ((unsigned long long)qb << 40);
       }
 #endif
     }
     __syncthreads();  // LDS images are reused by the next item
   }
+}
+
+// Persistent stream variant: same item lists as fa_fwd_f16_persistent_kernel,
+// walked as one continuous K/V tile stream (attention_stream).
+template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED>
+__global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_stream_kernel(FwdParams p) {
+  static_assert(WAVES == 8 && USE_M16 && SCHED == 1, "stream = 8-wave M16 ping-pong");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int x = blockIdx.x & 7, lcu = blockIdx.x >> 3, C = gridDim.x >> 3;
+  const int hx = (p.bh - x + 7) >> 3;  // heads h < bh with h % 8 == x
+  const int L = hx * p.nqb;
+  // rounds of C items in snake order; only the last round can be partial
+  const int full = L / C, part = L - full * C;
+  const int off_last = (full & 1) ? (C - 1 - lcu) : lcu;
+  const int n_items = full + (off_last < part ? 1 : 0);
+  auto item_at = [&](int r, int& bh, int& qb) {
+    const int pos = r * C + ((r & 1) ? (C - 1 - lcu) : lcu);
+    int lh, rank;
+    xcd_item(pos, hx, p.nqb, p.band, CAUSAL, lh, rank);
+    bh = x + 8 * lh;
+    qb = CAUSAL ? p.nqb - 1 - rank : rank;
+  };
+  attention_stream<M16<BN>, CAUSAL>(p, n_items, item_at, smem);
 }
 
 // Split-KV: workgroup id -> (split, item); items ordered as map_block.
@@ -213,7 +242,7 @@ struct Config {
   fa_config_info_t info;
   int mfma;   // 32 = v_mfma_f32_32x32x16_f16 loop, 16 = v_mfma_f32_16x16x32_f16 loop
   int sched;  // 0 = one barrier per tile, 1 = 8-wave ping-pong
-  int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent
+  int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent, 3 = persistent stream
   kernel_fn fn;
 };
 
@@ -223,11 +252,14 @@ constexpr kernel_fn pick_kernel() {
     return fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
   else if constexpr (SPL == 2)
     return fa_fwd_f16_persistent_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
+  else if constexpr (SPL == 3)
+    return fa_fwd_f16_stream_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
   else
     return fa_fwd_f16_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
 }
 
-// KIND: 0 = one workgroup per (head, query block), 1 = split-KV, 2 = persistent
+// KIND: 0 = one workgroup per (head, query block), 1 = split-KV, 2 = persistent,
+//       3 = persistent stream (K/V pipeline continuous across query blocks)
 #define FA_CFG(ID, W, BN_, C, KIND, M, SCHED, NAME)                                       \
   {{ID, 32 * (W), BN_, W, C, (KIND) == 1, 4 * (BN_) * ROW_BYTES, NAME}, M, SCHED, KIND, \
    pick_kernel<W, BN_, C, KIND, M, SCHED>()}
@@ -249,6 +281,8 @@ static const Config kConfigs[] = {
     FA_CFG(13, 4, 64, 1, 1, 16, 0, "bm128_bn64_w4_m16_causal_splitkv"),
     FA_CFG(14, 8, 64, 0, 2, 16, 1, "bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
     FA_CFG(15, 8, 64, 1, 2, 16, 1, "bm256_bn64_w8_m16_pingpong_persistent_causal"),
+    FA_CFG(16, 8, 64, 0, 3, 16, 1, "bm256_bn64_w8_m16_pingpong_stream_noncausal"),
+    FA_CFG(17, 8, 64, 1, 3, 16, 1, "bm256_bn64_w8_m16_pingpong_stream_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -324,7 +358,7 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   p.band = causal_band() > 0 ? causal_band() : (bh <= 64 ? 1 : 16);
   long long blocks = (long long)p.nqb * bh * num_splits;
   if (blocks > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
-  if (cfg.kind == 2) {
+  if (cfg.kind == 2 || cfg.kind == 3) {
     // one workgroup per CU, 8 per XCD group; never more than the items per XCD
     const long long per_xcd = (long long)((bh + 7) / 8) * p.nqb;
     const long long c = std::min<long long>(std::max(1, num_cus() / 8), per_xcd);
@@ -335,10 +369,10 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   return hipGetLastError() == hipSuccess ? FA_OK : FA_ERR_LAUNCH;
 }
 
-static int cfg_for(int waves, int bn, int causal, int mfma, int sched) {
+static int cfg_for(int waves, int bn, int causal, int mfma, int sched, int kind = 0) {
   for (int i = 0; i < kNumConfigs; ++i)
     if (kConfigs[i].info.waves == waves && kConfigs[i].info.block_n == bn &&
-        kConfigs[i].info.causal == causal && kConfigs[i].kind == 0 &&
+        kConfigs[i].info.causal == causal && kConfigs[i].kind == kind &&
         kConfigs[i].mfma == mfma && kConfigs[i].sched == sched)
       return i;
   return -1;
@@ -355,7 +389,10 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   const long long bh = (long long)batch * heads;
   const long long wg256 = bh * ((seq_len + 255) / 256);
   const int waves = wg256 >= 512 ? 8 : 4;
-  if (waves == 8) return cfg_for(8, 64, causal ? 1 : 0, 16, 1);  // 16x16x32 ping-pong
+  // 8 waves: 16x16x32 ping-pong, persistent (one workgroup per CU walking its
+  // XCD's items): removes the ~10 us dispatch gap between short causal
+  // workgroups (tools/timeline.py: CU busy 82.5% -> 95.2% at the headline shape)
+  if (waves == 8) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 2);
   return cfg_for(4, 64, causal ? 1 : 0, 32, 0);
 }
 
@@ -483,7 +520,7 @@ extern "C" const char* fa_version(void) { return "fa_mi355x 0.1 (gfx950)"; }
 #ifdef FA_STAMPS
 extern "C" int fa_debug_timeline(unsigned long long* out, int n) {
   if (n > FA_MAX_TIMELINE) n = FA_MAX_TIMELINE;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(fa::g_fa_timeline), (size_t)n * 24) == hipSuccess
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(fa::g_fa_timeline), (size_t)n * 32) == hipSuccess
              ? FA_OK
              : FA_ERR_HIP;
 }

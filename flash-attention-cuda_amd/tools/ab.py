@@ -22,6 +22,8 @@ ap.add_argument("--causal", action="store_true")
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--iters", type=int, default=30)
 ap.add_argument("--env", default="", help="label only")
+ap.add_argument("--data", default="uniform", choices=["uniform", "zeros", "small"],
+                help="uniform[-0.5,0.5] (default), all zeros, or uniform[-0.01,0.01]")
 ap.add_argument("--libs", default="", help="comma list of library variants: '' = libfa_mi355x.so, "
                 "X = libfa_mi355x_X.so; every config is timed against every variant")
 a = ap.parse_args()
@@ -30,6 +32,12 @@ g.manual_seed(3)
 shape = (a.batch, a.heads, a.seq, 128)
 q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5, generator=g)
            for _ in range(3))
+if a.data == "zeros":
+    for t in (q, k, v):
+        t.zero_()
+elif a.data == "small":
+    for t in (q, k, v):
+        t.mul_(0.02)
 o = torch.empty_like(q)
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 libs = {}
@@ -57,6 +65,6 @@ for _ in range(a.rounds):
         res[c].append(flops / (st.elapsed_time(en) / a.iters / 1e3) / 1e12)
 names = {c.id: c.name for c in fa.configs()}
 for c in cids:
-    print(json.dumps({"config": names[c[1]], "lib": c[0] or "base", "seq": a.seq, "batch": a.batch, "causal": a.causal,
+    print(json.dumps({"config": names[c[1]], "lib": c[0] or "base", "seq": a.seq, "batch": a.batch, "data": a.data, "causal": a.causal,
                       "median_tflops": round(statistics.median(res[c]), 1),
                       "min_tflops": round(min(res[c]), 1), "max_tflops": round(max(res[c]), 1)}))

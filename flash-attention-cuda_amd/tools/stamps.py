@@ -22,7 +22,7 @@ ap.add_argument("--causal", action="store_true")
 a = ap.parse_args()
 lib = fa.load_library()
 lib.fa_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-buf = (ctypes.c_ulonglong * 40)()
+buf = (ctypes.c_ulonglong * 64)()
 shape = (a.batch, a.heads, a.seq, 128)
 q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5) for _ in range(3))
 fa.flash_attention_fwd(q, k, v, a.causal, config=a.config)
@@ -31,9 +31,9 @@ lib.fa_debug_stamps(buf, 1)
 fa.flash_attention_fwd(q, k, v, a.causal, config=a.config)
 torch.cuda.synchronize()
 lib.fa_debug_stamps(buf, 1)
-tiles = (a.seq + 63) // 64
-iters = 64 * (tiles + 1)  # 64 workgroups x (n+1) loop iterations (non-causal)
-print("wave  mfma_blk  bar1  softmax  bar2  lds_write  (cycles per iteration, first 64 workgroups)")
+print("wave  mfma_blk  bar1  softmax  bar2  lds_write | issue_tile  (cycles per iteration, first 64 workgroups)")
 for w in range(8):
-    vals = [buf[w * 5 + i] / iters for i in range(5)]
-    print(w, " ".join(f"{x:9.0f}" for x in vals), f" total {sum(vals):.0f}")
+    iters = max(1, buf[w * 8 + 6])
+    vals = [buf[w * 8 + i] / iters for i in range(6)]
+    print(w, " ".join(f"{x:9.0f}" for x in vals[:5]), f" total {sum(vals[:5]):.0f} |", f"{vals[5]:.0f}",
+          f" iters {iters}")

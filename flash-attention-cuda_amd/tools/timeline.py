@@ -30,16 +30,19 @@ for _ in range(3):
     fa.flash_attention_fwd(q, k, v, a.causal, config=a.config)
 torch.cuda.synchronize()
 n = min(nblk, 65536)
-buf = (ctypes.c_ulonglong * (3 * n))()
+buf = (ctypes.c_ulonglong * (4 * n))()
 lib.fa_debug_timeline(buf, n)
-rows = [(buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]) for i in range(n)]
+rows = [(buf[4 * i], buf[4 * i + 1], buf[4 * i + 2]) for i in range(n)]
+clk = [buf[4 * i + 3] / max(1, buf[4 * i + 1] - buf[4 * i]) * 0.1 for i in range(n)]  # GHz
+clk.sort()
+print(f"  in-kernel clock (memtime/realtime): med {clk[len(clk)//2]:.3f} GHz p10 {clk[len(clk)//10]:.3f} p90 {clk[9*len(clk)//10]:.3f}")
 t0 = min(r[0] for r in rows)
 t1 = max(r[1] for r in rows)
 span = (t1 - t0) / 100.0  # us
 cu = collections.defaultdict(float)
 for s_, e_, hw in rows:
     h = hw & 0xFFFFFFFF
-    key = (hw >> 32, (h >> 13) & 7, (h >> 12) & 1, (h >> 8) & 15)  # xcc, se, sh, cu
+    key = ((hw >> 32) & 0xFF, (h >> 13) & 7, (h >> 12) & 1, (h >> 8) & 15)  # xcc, se, sh, cu
     cu[key] += (e_ - s_) / 100.0
 busy = sorted(cu.values())
 durs = sorted((e_ - s_) / 100.0 for s_, e_, _ in rows)
@@ -50,3 +53,28 @@ print(f"  CU busy: mean {sum(busy)/len(busy):.1f} us ({100*sum(busy)/len(busy)/s
 print(f"  workgroup duration: min {durs[0]:.2f} med {durs[len(durs)//2]:.2f} max {durs[-1]:.2f} us")
 print(f"  last 1% of workgroups end after {ends[int(0.99*len(ends))]:.1f} us; "
       f"first end {ends[0]:.1f} us")
+
+# per-CU gaps between consecutive workgroups, and duration vs query block
+percu = collections.defaultdict(list)
+byqb = collections.defaultdict(list)
+for s_, e_, hw in rows:
+    h = hw & 0xFFFFFFFF
+    percu[((hw >> 32) & 0xFF, (h >> 13) & 7, (h >> 12) & 1, (h >> 8) & 15)].append((s_, e_))
+    byqb[(hw >> 40) & 0xFFFF].append((e_ - s_) / 100.0)
+gaps = []
+for lst in percu.values():
+    lst.sort()
+    gaps += [(b[0] - a_[1]) / 100.0 for a_, b in zip(lst, lst[1:])]
+gaps.sort()
+if gaps:
+    print(f"  gap between consecutive WGs on a CU: mean {sum(gaps)/len(gaps):.2f} "
+          f"med {gaps[len(gaps)//2]:.2f} p90 {gaps[int(0.9*len(gaps))]:.2f} us")
+xs = sorted(byqb)
+pts = [(qb + 1, sum(v) / len(v)) for qb, v in ((x, byqb[x]) for x in xs)]
+if len(pts) > 2:
+    n_ = len(pts)
+    mx = sum(p_[0] for p_ in pts) / n_
+    my = sum(p_[1] for p_ in pts) / n_
+    sl = sum((p_[0] - mx) * (p_[1] - my) for p_ in pts) / sum((p_[0] - mx) ** 2 for p_ in pts)
+    print(f"  duration ~ {my - sl * mx:.2f} us + {sl:.3f} us x (qb+1)   [causal: per 256-row key step]")
+    print("  qb:dur " + " ".join(f"{x}:{sum(byqb[x])/len(byqb[x]):.1f}" for x in xs[:32]))
