@@ -480,7 +480,13 @@ struct M16 {
       for (int cb = 0; cb < NKB; ++cb)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          pf[b][cb >> 1][4 * (cb & 1) + i] = (f16)__builtin_amdgcn_exp2f(s[b][cb][i]);
+        {
+          const float e = __builtin_amdgcn_exp2f(s[b][cb][i]);
+#ifdef FA_ROWSUM_VALU
+          lacc[b][0] += e;  // this lane's partial row sum (4 lanes per row)
+#endif
+          pf[b][cb >> 1][4 * (cb & 1) + i] = (f16)e;
+        }
   }
   template <bool CAUSAL>
   __device__ __forceinline__ void softmax(int kv0, int kv_hi, int qw, float /*c*/, bool need_mask) {
@@ -509,10 +515,21 @@ struct M16 {
       for (int cb = 0; cb < NKB; ++cb)
 #pragma unroll
         for (int i = (cb == 0 ? 1 : 0); i < 4; ++i) m = fmaxf(m, s[b][cb][i]);
+#ifdef FA_ROWMAX_ALWAYS
       mx[b] = max_xor32(max_xor16(m));
+#else
+      // a row's max exceeds the threshold iff one of its 4 lanes' partial
+      // maxima does: the cross-lane reduction is only needed on the rare
+      // (wave-uniform) rescale path
+      mx[b] = m;
+#endif
       grow |= mx[b] > RESCALE_LOG2;
     }
     if (__any(grow)) {
+#ifndef FA_ROWMAX_ALWAYS
+#pragma unroll
+      for (int b = 0; b < 2; ++b) mx[b] = max_xor32(max_xor16(mx[b]));
+#endif
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         // first tile: centre on the max; later: only ever move m_ref up.
@@ -553,9 +570,11 @@ struct M16 {
           acc[b][e] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[b][u], acc[b][e], 0, 0, 0);
       }
       // row sums of the same fp16 P: every register of lacc[b] = l for q = lane&15
+#ifndef FA_ROWSUM_VALU
 #pragma unroll
       for (int b = 0; b < 2; ++b)
         lacc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, pf[b][u], lacc[b], 0, 0, 0);
+#endif
     }
   }
   // the ping-pong MFMA block: PV(V_{k-1}) then QK^T(K_k); the barrier keeps the
@@ -606,10 +625,17 @@ struct M16 {
     pv(vb);
   }
 
+  __device__ __forceinline__ float row_sum(int b) const {
+#ifdef FA_ROWSUM_VALU
+    return sum_xor32(sum_xor16(lacc[b][0]));
+#else
+    return lacc[b][0];  // already the full row sum (MFMA over all keys)
+#endif
+  }
   __device__ __forceinline__ void store_o(__amdgpu_buffer_rsrc_t ro, int qw) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
-      const float lt = lacc[b][0];  // already the full row sum (MFMA over all keys)
+      const float lt = row_sum(b);  // already the full row sum (MFMA over all keys)
       const float inv = lt > 0.f ? 1.0f / lt : 0.f;
       const int rowb = (qw + 16 * b + r16) * ROW_BYTES;
 #pragma unroll
@@ -626,7 +652,7 @@ struct M16 {
                                                 int S, float /*scale*/) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
-      const float lt = lacc[b][0];
+      const float lt = row_sum(b);
       const int q = qw + 16 * b + r16;
 #pragma unroll
       for (int e = 0; e < 8; ++e) buf_store16f(rpo, q * HD * 4 + 4 * (16 * e + 4 * g), acc[b][e]);
