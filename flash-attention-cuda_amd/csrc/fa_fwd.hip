@@ -254,6 +254,7 @@ constexpr kernel_fn pick_kernel() {
     return fa_fwd_f16_persistent_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
   else if constexpr (SPL == 3)
     return fa_fwd_f16_stream_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
+
   else
     return fa_fwd_f16_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
 }
@@ -261,8 +262,8 @@ constexpr kernel_fn pick_kernel() {
 // KIND: 0 = one workgroup per (head, query block), 1 = split-KV, 2 = persistent,
 //       3 = persistent stream (K/V pipeline continuous across query blocks)
 #define FA_CFG(ID, W, BN_, C, KIND, M, SCHED, NAME)                                       \
-  {{ID, 32 * (W), BN_, W, C, (KIND) == 1, 4 * (BN_) * ROW_BYTES, NAME}, M, SCHED, KIND, \
-   pick_kernel<W, BN_, C, KIND, M, SCHED>()}
+  {{ID, 32 * (W), BN_, W, C, (KIND) == 1, 4 * (BN_) * ROW_BYTES, NAME}, \
+   M, SCHED, KIND, pick_kernel<W, BN_, C, KIND, M, SCHED>()}
 
 static const Config kConfigs[] = {
     FA_CFG(0, 4, 64, 0, 0, 32, 0, "bm128_bn64_w4_m32_noncausal"),
@@ -384,16 +385,16 @@ using namespace fa;
 
 extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   // Tier table re-derived for 256 CUs (ref :620-661 picks by seq >= 2048 on
-  // 58 SMs).  256-row workgroups (8 waves) halve the K/V re-reads per query
-  // row; use them once they still give >= 2 workgroups per CU.
+  // 58 SMs), from tools/small_s.py and tools/sweep.py on the box:
+  //  * 8-wave persistent ping-pong (256 rows / workgroup) once there are two
+  //    256-row items per CU, or one per CU without a mask (S=2048 B=1 H=32
+  //    non-causal: 1015 vs 873 TFLOP/s);
+  //  * otherwise 4-wave 16x16x32 (128 rows), which keeps more CUs busy on the
+  //    short, latency-bound launches (S <= 2048 causal at B=1 H=32).
   const long long bh = (long long)batch * heads;
   const long long wg256 = bh * ((seq_len + 255) / 256);
-  const int waves = wg256 >= 512 ? 8 : 4;
-  // 8 waves: 16x16x32 ping-pong, persistent (one workgroup per CU walking its
-  // XCD's items): removes the ~10 us dispatch gap between short causal
-  // workgroups (tools/timeline.py: CU busy 82.5% -> 95.2% at the headline shape)
-  if (waves == 8) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 2);
-  return cfg_for(4, 64, causal ? 1 : 0, 32, 0);
+  if (wg256 >= 512 || (!causal && wg256 >= 256)) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 2);
+  return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
 }
 
 extern "C" int fa_fwd_f16_config(const void* q, const void* k, const void* v, void* o,
