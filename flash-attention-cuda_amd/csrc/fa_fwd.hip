@@ -169,29 +169,6 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(Fw
   }
 }
 
-// Persistent stream variant: same item lists as fa_fwd_f16_persistent_kernel,
-// walked as one continuous K/V tile stream (attention_stream).
-template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED>
-__global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_stream_kernel(FwdParams p) {
-  static_assert(WAVES == 8 && USE_M16 && SCHED == 1, "stream = 8-wave M16 ping-pong");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int x = blockIdx.x & 7, lcu = blockIdx.x >> 3, C = gridDim.x >> 3;
-  const int hx = (p.bh - x + 7) >> 3;  // heads h < bh with h % 8 == x
-  const int L = hx * p.nqb;
-  // rounds of C items in snake order; only the last round can be partial
-  const int full = L / C, part = L - full * C;
-  const int off_last = (full & 1) ? (C - 1 - lcu) : lcu;
-  const int n_items = full + (off_last < part ? 1 : 0);
-  auto item_at = [&](int r, int& bh, int& qb) {
-    const int pos = r * C + ((r & 1) ? (C - 1 - lcu) : lcu);
-    int lh, rank;
-    xcd_item(pos, hx, p.nqb, p.band, CAUSAL, lh, rank);
-    bh = x + 8 * lh;
-    qb = CAUSAL ? p.nqb - 1 - rank : rank;
-  };
-  attention_stream<M16<BN>, CAUSAL>(p, n_items, item_at, smem);
-}
-
 // Split-KV: workgroup id -> (split, item); items ordered as map_block.
 template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED>
 __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_splitkv_kernel(FwdParams p) {
@@ -242,7 +219,7 @@ struct Config {
   fa_config_info_t info;
   int mfma;   // 32 = v_mfma_f32_32x32x16_f16 loop, 16 = v_mfma_f32_16x16x32_f16 loop
   int sched;  // 0 = one barrier per tile, 1 = 8-wave ping-pong
-  int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent, 3 = persistent stream
+  int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent
   kernel_fn fn;
 };
 
@@ -252,15 +229,13 @@ constexpr kernel_fn pick_kernel() {
     return fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
   else if constexpr (SPL == 2)
     return fa_fwd_f16_persistent_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
-  else if constexpr (SPL == 3)
-    return fa_fwd_f16_stream_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
+
 
   else
     return fa_fwd_f16_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
 }
 
-// KIND: 0 = one workgroup per (head, query block), 1 = split-KV, 2 = persistent,
-//       3 = persistent stream (K/V pipeline continuous across query blocks)
+// KIND: 0 = one workgroup per (head, query block), 1 = split-KV, 2 = persistent
 #define FA_CFG(ID, W, BN_, C, KIND, M, SCHED, NAME)                                       \
   {{ID, 32 * (W), BN_, W, C, (KIND) == 1, 4 * (BN_) * ROW_BYTES, NAME}, \
    M, SCHED, KIND, pick_kernel<W, BN_, C, KIND, M, SCHED>()}
@@ -282,8 +257,6 @@ static const Config kConfigs[] = {
     FA_CFG(13, 4, 64, 1, 1, 16, 0, "bm128_bn64_w4_m16_causal_splitkv"),
     FA_CFG(14, 8, 64, 0, 2, 16, 1, "bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
     FA_CFG(15, 8, 64, 1, 2, 16, 1, "bm256_bn64_w8_m16_pingpong_persistent_causal"),
-    FA_CFG(16, 8, 64, 0, 3, 16, 1, "bm256_bn64_w8_m16_pingpong_stream_noncausal"),
-    FA_CFG(17, 8, 64, 1, 3, 16, 1, "bm256_bn64_w8_m16_pingpong_stream_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -359,7 +332,7 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   p.band = causal_band() > 0 ? causal_band() : (bh <= 64 ? 1 : 16);
   long long blocks = (long long)p.nqb * bh * num_splits;
   if (blocks > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
-  if (cfg.kind == 2 || cfg.kind == 3) {
+  if (cfg.kind == 2) {
     // one workgroup per CU, 8 per XCD group; never more than the items per XCD
     const long long per_xcd = (long long)((bh + 7) / 8) * p.nqb;
     const long long c = std::min<long long>(std::max(1, num_cus() / 8), per_xcd);

@@ -129,7 +129,7 @@ __device__ __forceinline__ float ninf() { return -__builtin_inff(); }
 // diagnostic build only (lib/libfa_mi355x_stamps.so): per-wave cycles spent in
 // [MFMA block, barrier after it, softmax block, barrier after it, LDS tile write], summed over
 // the first 64 workgroups.  Never part of the product library.
-__device__ unsigned long long g_fa_stamps[8][8];  // 5 phases, issue_tile, iterations, spare
+__device__ unsigned long long g_fa_stamps[8][12];  // 5 phases, issue_tile, iterations, prologue, epilogue, items
 // per-workgroup timeline: {start, end (s_memrealtime, 100 MHz), hw_id | xcc_id << 32 | qb << 40,
 //                          shader cycles (s_memtime) start..end}
 constexpr int FA_MAX_TIMELINE = 65536;
@@ -188,14 +188,19 @@ struct M32 {
     have_ref = false;
   }
   // Q (B operand of S^T): lane holds c * Q[qw + r][16t + 8h .. +7]  (fp16)
+  __device__ __forceinline__ void issue_q(__amdgpu_buffer_rsrc_t rq, int qw) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) qf[t] = buf_load16(rq, (qw + r) * ROW_BYTES + (2 * t + h) * 16);
+  }
+  __device__ __forceinline__ void scale_q() {
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[t][j] = (f16)((float)qf[t][j] * c);
+  }
   __device__ __forceinline__ void load_q(__amdgpu_buffer_rsrc_t rq, int qw) {
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      f16x8 x = buf_load16(rq, (qw + r) * ROW_BYTES + (2 * t + h) * 16);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = (f16)((float)x[j] * c);
-      qf[t] = x;
-    }
+    issue_q(rq, qw);
+    scale_q();
   }
   // staging: 8 consecutive lanes = two rows of opposite parity x 4 chunks
   // (conflict-free ds_write_b128 into image A)
@@ -426,24 +431,6 @@ struct M16 {
   __device__ __forceinline__ void load_q(__amdgpu_buffer_rsrc_t rq, int qw) {
     issue_q(rq, qw);
     scale_q();
-  }
-  // persistent stream: the running max / QK^T bias restart before the next
-  // query block's first QK^T; O and l restart once O has been stored
-  __device__ __forceinline__ void reset_max() {
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      negm[b] = f32x4{};
-      m_ref[b] = 0.f;
-    }
-    have_ref = false;
-  }
-  __device__ __forceinline__ void reset_acc() {
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[b][e] = f32x4{};
-      lacc[b] = f32x4{};
-    }
   }
   // K staging: natural row-major lanes (8 lanes = 8 chunks of one row: conflict-free
   // writes into image B); V staging as M32 (image A)
@@ -822,9 +809,12 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   }
   const int n = kv_hi > kv_lo ? (kv_hi - kv_lo + BN - 1) / BN : 0;
 
+#ifdef FA_STAMPS
+  const unsigned long long t_in = __builtin_amdgcn_s_memtime();
+#endif
   Pol pol;
   pol.init(lane, p.c);
-  pol.load_q(make_rsrc(Qh, S * ROW_BYTES), qw);
+  pol.issue_q(make_rsrc(Qh, S * ROW_BYTES), qw);  // scaled once K_0 / tile 0 are in flight
 
   char* kbuf0 = smem;
   char* vbuf0 = smem + 2 * TILE_BYTES;
@@ -852,18 +842,26 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     }
   };
 
-  // prologue: K_0 by everyone; group B also issues tile 0 (written in half-step 0)
+  // prologue: Q, K_0 (everyone) and tile 0 (group B, written in half-step 0)
+  // are all in flight together, so the item start pays one memory latency
   {
     const auto rk = make_rsrc(Kh + (size_t)kv_lo * HD, (kv_hi - kv_lo) * ROW_BYTES);
+    f16x8 k0[NCH];
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
-      kst[i] = buf_load16(rk, (kr0 + 4 * WAVES * i) * ROW_BYTES + kc * 16);
+      k0[i] = buf_load16(rk, (kr0 + 4 * WAVES * i) * ROW_BYTES + kc * 16);
+    if (grp == 1 && n > 0) issue_tile(0);
+    pol.scale_q();
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
-      *reinterpret_cast<f16x8*>(kbuf0 + Pol::k_lds(kr0 + 4 * WAVES * i, kc)) = kst[i];
+      *reinterpret_cast<f16x8*>(kbuf0 + Pol::k_lds(kr0 + 4 * WAVES * i, kc)) = k0[i];
   }
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // Q and K_0 retired before the loop (see attention_tile_loop)
-  if (grp == 1 && n > 0) issue_tile(0);
+  // Q and K_0 retired before the loop (see attention_tile_loop); group B's
+  // tile-0 loads may stay in flight (they are the 2*NCH most recent)
+  if (grp == 1)
+    __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * NCH));
+  else
+    __builtin_amdgcn_s_waitcnt(0x0F70);
   __syncthreads();
 
   const float c = p.c;
@@ -893,7 +891,8 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     __syncthreads();
   }
 #ifdef FA_STAMPS
-  unsigned long long st_acc[7] = {0, 0, 0, 0, 0, 0, 0}, st0, st01, st1, st2, st3, st4;
+  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 1}, st0, st01, st1, st2, st3, st4;
+  st_acc[7] = __builtin_amdgcn_s_memtime() - t_in;
 #define FA_STAMP(v)                                                                   \
   do {                                                                                \
     __builtin_amdgcn_sched_barrier(0);                                                \
@@ -937,10 +936,8 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   }
   if (grp == 0) __syncthreads();
 #ifdef FA_STAMPS
-  if (lane == 0 && blockIdx.x < 64)
-    for (int i = 0; i < 7; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
+  const unsigned long long t_le = __builtin_amdgcn_s_memtime();
 #endif
-#undef FA_STAMP
 
   if constexpr (!SPLIT) {
     pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);
@@ -949,229 +946,15 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     pol.store_partial(make_rsrc(p.part_o + prow0 * HD, S * HD * 4), p.part_ml + prow0 * 2, qw, S,
                       p.scale);
   }
-}
-
-
-// ---------------------------------------------------------------------------
-// Persistent STREAM ping-pong: one workgroup per CU walks its list of query
-// blocks ("items") as ONE continuous tile stream.  The K/V pipeline never
-// drains between items: the tile after an item's last one carries the next
-// item's K_0, the next item's Q is loaded into the Q registers during the
-// softmax phase that follows the item's last QK^T, and the finished item's O
-// is normalised and stored during the softmax phase of the next item's first
-// tile.  Same per-tile schedule as attention_pingpong (group B one half-step
-// behind A, MFMA phase at s_setprio 1).
-//
-// item_at(i, bh, qb): the i-th item of this workgroup, i < n_items.
-template <class Pol, bool CAUSAL, class ItemAt>
-__device__ __forceinline__ void attention_stream(const FwdParams& p, int n_items, ItemAt item_at,
-                                                 char* smem) {
-  constexpr int WAVES = 8;
-  constexpr int BN = Pol::BN;
-  constexpr int NT = WAVES * 64;
-  constexpr int BM = WAVES * 32;
-  constexpr int TILE_BYTES = BN * ROW_BYTES;
-  constexpr int NCH = (BN * 16) / NT;
-  static_assert((BN * 16) % NT == 0, "tile chunks must divide evenly");
-  if (n_items <= 0) return;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wave >> 2;  // 0 = A, 1 = B (wave-uniform)
-  const int S = p.seq_len;
-
-  // wave-uniform item descriptor
-  struct Item {
-    int bh, q0, kv_hi, n;
-  };
-  auto info = [&](int i) {
-    Item it{0, 0, 0, 0};
-    if (i < n_items) {
-      int bh, qb;
-      item_at(i, bh, qb);
-      it.bh = bh;
-      it.q0 = qb * BM;
-      it.kv_hi = CAUSAL ? min(it.q0 + BM, S) : S;
-      it.n = (it.kv_hi + BN - 1) / BN;
-    }
-    return it;
-  };
-  auto head = [&](const f16* base, int bh) { return base + (size_t)bh * (size_t)S * HD; };
-
-  Pol pol;
-  pol.init(lane, p.c);
-
-  char* kbuf0 = smem;
-  char* vbuf0 = smem + 2 * TILE_BYTES;
-  const int kr0 = pol.k_stage_row(wave), kc = pol.k_stage_ch();
-  const int vr0 = pol.v_stage_row(wave), vc = pol.v_stage_ch();
-  f16x8 kst[NCH], vst[NCH];
-
-  // load cursor: global tile lt = (K of the following tile, V_lk of item lr).
-  // Pointers advance by one tile per issue; the per-item math (head offsets,
-  // item decode) runs only at item switches.
-  int lr = 0, lk = 0, lt = 0;
-  Item li = info(0), ln = info(1);
-  const f16* vptr = head(p.v, li.bh);
-  int vbytes = li.kv_hi * ROW_BYTES;
-  const f16* kptr;
-  int kbytes;
-  auto k_for = [&]() {  // K rows of the tile after (item lr, tile lk)
-    if (lk + 1 < li.n) {
-      kptr = head(p.k, li.bh) + (size_t)(lk + 1) * BN * HD;
-      kbytes = (li.kv_hi - (lk + 1) * BN) * ROW_BYTES;
-    } else {  // next item's K_0 (absent: 0 bytes -> zeros)
-      kptr = head(p.k, ln.bh);
-      kbytes = ln.kv_hi * ROW_BYTES;
-    }
-  };
-  k_for();
-  auto issue_tile = [&]() {
-    const auto rk = make_rsrc(kptr, kbytes);
-    const auto rv = make_rsrc(vptr, vbytes);
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      kst[i] = buf_load16(rk, (kr0 + 4 * WAVES * i) * ROW_BYTES + kc * 16);
-      vst[i] = buf_load16(rv, (vr0 + 4 * WAVES * i) * ROW_BYTES + vc * 16);
-    }
-    ++lt;
-    if (++lk < li.n) {
-      vptr += BN * HD;
-      vbytes -= BN * ROW_BYTES;
-      if (lk + 1 < li.n) {
-        kptr += BN * HD;
-        kbytes -= BN * ROW_BYTES;
-      } else {
-        k_for();
-      }
-    } else {
-      lk = 0;
-      ++lr;
-      li = ln;
-      ln = info(lr + 1);
-      vptr = head(p.v, li.bh);
-      vbytes = li.kv_hi * ROW_BYTES;
-      k_for();
-    }
-  };
-  auto write_tile = [&](int t) {
-    char* kb = kbuf0 + ((t + 1) & 1) * TILE_BYTES;
-    char* vb = vbuf0 + (t & 1) * TILE_BYTES;
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      *reinterpret_cast<f16x8*>(kb + Pol::k_lds(kr0 + 4 * WAVES * i, kc)) = kst[i];
-      *reinterpret_cast<f16x8*>(vb + Pol::v_lds(vr0 + 4 * WAVES * i, vc)) = vst[i];
-    }
-  };
-
-  // compute cursor: step G does PV of tile G-1 and QK^T of tile G (= tile ck of item cr)
-  int cr = 0, ck = 0;
-  Item ci = li;
-  Item pi = ci;  // item whose O is still in the accumulators
-
-  // prologue: Q and K_0 of the first item; group B also loads tile 0
-  pol.load_q(make_rsrc(head(p.q, ci.bh), S * ROW_BYTES), ci.q0 + wave * 32);
-  {
-    const auto rk = make_rsrc(head(p.k, ci.bh), ci.kv_hi * ROW_BYTES);
-#pragma unroll
-    for (int i = 0; i < NCH; ++i)
-      kst[i] = buf_load16(rk, (kr0 + 4 * WAVES * i) * ROW_BYTES + kc * 16);
-#pragma unroll
-    for (int i = 0; i < NCH; ++i)
-      *reinterpret_cast<f16x8*>(kbuf0 + Pol::k_lds(kr0 + 4 * WAVES * i, kc)) = kst[i];
-  }
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-  if (grp == 1) issue_tile();
-  __syncthreads();
-  if (grp == 1) {
-    write_tile(0);
-    __syncthreads();
-  }
-
-  const float c = p.c;
-  bool have_p = false;  // this wave holds a P tile whose PV is still due
 #ifdef FA_STAMPS
-  unsigned long long st_acc[7] = {0, 0, 0, 0, 0, 0, 0}, st0, st01, st1, st2, st25, st3, st4;
-#define FA_STAMP(v)                                                                   \
-  do {                                                                                \
-    __builtin_amdgcn_sched_barrier(0);                                                \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");         \
-    __builtin_amdgcn_sched_barrier(0);                                                \
-  } while (0)
-#else
-#define FA_STAMP(v) \
-  do {              \
-  } while (0)
-#endif
-  for (int G = 0;; ++G) {
-    const bool live = cr < n_items;
-    const int qw = ci.q0 + wave * 32;
-    const bool do_qk = live && (!CAUSAL || ck * BN <= qw + 31);
-    const bool issued = lr < n_items;
-    const int t = lt;
-    FA_STAMP(st0);
-    if (issued) issue_tile();
-    FA_STAMP(st01);
-    if constexpr (true) __builtin_amdgcn_s_setprio(1);
-    pol.mfma_block(kbuf0 + (G & 1) * TILE_BYTES, vbuf0 + ((G - 1) & 1) * TILE_BYTES, have_p, do_qk);
-    __builtin_amdgcn_s_setprio(0);
-    FA_STAMP(st1);
-    __syncthreads();
-    FA_STAMP(st2);
-    if (ck == 0 && G > 0) {
-      // the accumulators hold the finished O of the previous item
-      pol.store_o(make_rsrc(head(p.o, pi.bh), S * ROW_BYTES), pi.q0 + wave * 32);
-      pol.reset_acc();
-    }
-    if (do_qk) {
-      const int kv0 = ck * BN;
-      const bool need_mask = (kv0 + BN > ci.kv_hi) || (CAUSAL && kv0 + BN - 1 > qw);
-      pol.template softmax<CAUSAL>(kv0, ci.kv_hi, qw, c, need_mask);
-    }
-    have_p = do_qk;
-    FA_STAMP(st25);
-    const bool last = live && ck + 1 == ci.n;
-    if (last) pol.reset_max();  // the next QK^T (next item) starts a fresh running max
-    if (last && cr + 1 < n_items) {
-      // next item's Q: QK^T of this item is done, its first QK^T is next step.
-      // Loads and prescale on one path, so the waitcnt pass sees Q retired.
-      int nbh, nqb;
-      item_at(cr + 1, nbh, nqb);
-      pol.issue_q(make_rsrc(head(p.q, nbh), S * ROW_BYTES), nqb * BM + wave * 32);
-      if (issued) write_tile(t);
-      pol.scale_q();
-    } else if (issued) {
-      write_tile(t);
-    }
-    FA_STAMP(st3);
-    __syncthreads();
-    FA_STAMP(st4);
-#ifdef FA_STAMPS
-    st_acc[0] += st1 - st01;
-    st_acc[1] += st2 - st1;
-    st_acc[2] += st25 - st2;
-    st_acc[3] += st4 - st3;
-    st_acc[4] += st3 - st25;
-    st_acc[5] += st01 - st0;
-    st_acc[6] += 1;
-#endif
-    if (!live) break;
-    if (last) {
-      pi = ci;
-      ++cr;
-      ck = 0;
-      ci = info(cr);
-    } else {
-      ++ck;
-    }
-  }
-  if (grp == 0) __syncthreads();
-#ifdef FA_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);  // stores issued and retired
+  st_acc[8] = __builtin_amdgcn_s_memtime() - t_le;
   if (lane == 0 && blockIdx.x < 64)
-    for (int i = 0; i < 7; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
+    for (int i = 0; i < 10; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
 #endif
 #undef FA_STAMP
 }
+
+
 
 }  // namespace fa

@@ -22,7 +22,7 @@ ap.add_argument("--causal", action="store_true")
 a = ap.parse_args()
 lib = fa.load_library()
 lib.fa_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-buf = (ctypes.c_ulonglong * 64)()
+buf = (ctypes.c_ulonglong * 96)()
 shape = (a.batch, a.heads, a.seq, 128)
 q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5) for _ in range(3))
 fa.flash_attention_fwd(q, k, v, a.causal, config=a.config)
@@ -31,9 +31,11 @@ lib.fa_debug_stamps(buf, 1)
 fa.flash_attention_fwd(q, k, v, a.causal, config=a.config)
 torch.cuda.synchronize()
 lib.fa_debug_stamps(buf, 1)
-print("wave  mfma_blk  bar1  softmax  bar2  lds_write | issue_tile  (cycles per iteration, first 64 workgroups)")
+print("wave  mfma_blk  bar1  softmax  bar2  lds_write | issue_tile  (cycles per iteration, first 64 "
+      "workgroups) | prologue  epilogue (cycles per item)")
 for w in range(8):
-    iters = max(1, buf[w * 8 + 6])
-    vals = [buf[w * 8 + i] / iters for i in range(6)]
+    iters = max(1, buf[w * 12 + 6])
+    items = max(1, buf[w * 12 + 9])
+    vals = [buf[w * 12 + i] / iters for i in range(6)]
     print(w, " ".join(f"{x:9.0f}" for x in vals[:5]), f" total {sum(vals[:5]):.0f} |", f"{vals[5]:.0f}",
-          f" iters {iters}")
+          f" iters {iters} | {buf[w * 12 + 7] / items:.0f} {buf[w * 12 + 8] / items:.0f}  items {items}")

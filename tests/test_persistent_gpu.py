@@ -1,12 +1,12 @@
-"""Persistent kernels (kind 2 = one item at a time, kind 3 = continuous K/V
-stream across items): shapes where every workgroup walks SEVERAL query blocks,
-including ragged sequence lengths, head counts that are not a multiple of the
-8 XCD groups, and single-tile items.
+"""Persistent kernel (one workgroup per CU walking its XCD's query blocks):
+shapes where every workgroup walks SEVERAL query blocks, including ragged
+sequence lengths, head counts that are not a multiple of the 8 XCD groups,
+and single-tile items.
 
-Both persistent kernels run exactly the per-tile arithmetic of the
-one-workgroup-per-item ping-pong kernel (configs 8/9) in the same order, so
-their outputs must be bit-identical to it; sampled heads are also checked
-against the oracle (reference cpu_attention restatement) at the 1e-3 gate.
+It runs exactly the per-tile arithmetic of the one-workgroup-per-item
+ping-pong kernel (configs 8/9) in the same order, so its output must be
+bit-identical to it; sampled heads are also checked against the oracle
+(reference cpu_attention restatement) at the 1e-3 gate.
 """
 import numpy as np
 import pytest
@@ -57,7 +57,7 @@ SHAPES = [
 
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
-@pytest.mark.parametrize("kind", ["persistent", "stream"])
+@pytest.mark.parametrize("kind", ["persistent"])
 def test_persistent_bit_identical(kind, shape, causal):
     fa = _fa()
     b, h, s = shape
