@@ -314,7 +314,8 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
             "traffic": traffic,
-            "kernel": f"fa_fwd_f16_kernel ({cfg_name})",
+            "kernel": ("fa_fwd_f16_persistent_kernel" if "persistent" in cfg_name
+                       else "fa_fwd_f16_kernel") + f" ({cfg_name})",
             "avg_launch_ms": round(avg_launch_ms, 4),
             "flops_per_launch": flops_per_launch,
             "algorithmic_bytes_per_launch": algorithmic_bytes(b_local, H, S, HEAD_DIM),

@@ -12,7 +12,7 @@ import json
 import os
 import sys
 
-KERNEL = "fa_fwd_f16_kernel"
+KERNEL = "fa_fwd_f16"  # fa_fwd_f16_kernel or fa_fwd_f16_persistent_kernel
 WORKLOAD = "b64_h32_s4096_d128_causal"
 
 
