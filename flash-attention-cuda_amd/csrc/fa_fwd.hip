@@ -67,10 +67,13 @@ __device__ __forceinline__ void map_block(int id, int nblk, int nqb, int bh_coun
 
 // SCHED: 0 = one-barrier-per-tile loop (any wave count), 1 = 8-wave ping-pong
 // (MFMA phase at s_setprio 1), 2 = ping-pong without the priority raise
-template <int WAVES, int BN, bool CAUSAL, bool SPLIT, bool USE_M16, int SCHED>
+// BF16: Q/K/V/O and the MFMA operands are bf16 (16x16x32 policy only)
+template <int WAVES, int BN, bool CAUSAL, bool SPLIT, bool USE_M16, int SCHED, bool BF16 = false>
 __device__ __forceinline__ void run_tile_loop(const FwdParams& p, int bh, int qb, int split,
                                               char* smem) {
-  using Pol = typename std::conditional<USE_M16, M16<BN>, M32<BN>>::type;
+  static_assert(USE_M16 || !BF16, "bf16 runs on the 16x16x32 policy");
+  using Pol = typename std::conditional<USE_M16, M16<BN, typename std::conditional<BF16, __bf16, f16>::type>,
+                                        M32<BN>>::type;
   if constexpr (SCHED == 1 || SCHED == 2) {
     static_assert(WAVES == 8, "ping-pong needs two groups of four waves");
     attention_pingpong<Pol, CAUSAL, SPLIT, SCHED == 1>(p, bh, qb, split, smem);
@@ -79,7 +82,7 @@ __device__ __forceinline__ void run_tile_loop(const FwdParams& p, int bh, int qb
   }
 }
 
-template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED>
+template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED, bool BF16 = false>
 __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 #ifdef FA_STAMPS
@@ -88,7 +91,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_kernel(FwdParams p) 
 #endif
   int qb, bh;
   map_block(blockIdx.x, gridDim.x, p.nqb, p.bh, p.band, CAUSAL, qb, bh);
-  run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED>(p, bh, qb, 0, smem);
+  run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED, BF16>(p, bh, qb, 0, smem);
 #ifdef FA_STAMPS
   if (threadIdx.x == 0 && blockIdx.x < FA_MAX_TIMELINE) {
     unsigned hw, xcc;
@@ -133,7 +136,7 @@ __device__ __forceinline__ void xcd_item(int j, int hx, int nqb, int band, bool 
   }
 }
 
-template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED>
+template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED, bool BF16 = false>
 __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int x = blockIdx.x & 7, lcu = blockIdx.x >> 3, C = gridDim.x >> 3;
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(Fw
       const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
       const unsigned long long c_start = __builtin_amdgcn_s_memtime();
 #endif
-      run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED>(p, bh, qb, 0, smem);
+      run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED, BF16>(p, bh, qb, 0, smem);
 #ifdef FA_STAMPS
       const int rec = bh * p.nqb + qb;
       if (threadIdx.x == 0 && rec < FA_MAX_TIMELINE) {
@@ -223,22 +226,22 @@ struct Config {
   kernel_fn fn;
 };
 
-template <int W, int BN_, int C, int SPL, int M, int SCHED>
+template <int W, int BN_, int C, int SPL, int M, int SCHED, int DT>
 constexpr kernel_fn pick_kernel() {
   if constexpr (SPL == 1)
     return fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
   else if constexpr (SPL == 2)
-    return fa_fwd_f16_persistent_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
-
-
+    return fa_fwd_f16_persistent_kernel<W, BN_, (C != 0), (M == 16), SCHED, DT == 1>;
   else
-    return fa_fwd_f16_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
+    return fa_fwd_f16_kernel<W, BN_, (C != 0), (M == 16), SCHED, DT == 1>;
 }
 
 // KIND: 0 = one workgroup per (head, query block), 1 = split-KV, 2 = persistent
-#define FA_CFG(ID, W, BN_, C, KIND, M, SCHED, NAME)                                       \
-  {{ID, 32 * (W), BN_, W, C, (KIND) == 1, 4 * (BN_) * ROW_BYTES, NAME}, \
-   M, SCHED, KIND, pick_kernel<W, BN_, C, KIND, M, SCHED>()}
+// DT: 0 = fp16, 1 = bf16 (FA_DTYPE_*)
+#define FA_CFG_T(ID, W, BN_, C, KIND, M, SCHED, DT, NAME)                              \
+  {{ID, 32 * (W), BN_, W, C, (KIND) == 1, 4 * (BN_) * ROW_BYTES, NAME, DT}, M, SCHED, KIND, \
+   pick_kernel<W, BN_, C, KIND, M, SCHED, DT>()}
+#define FA_CFG(ID, W, BN_, C, KIND, M, SCHED, NAME) FA_CFG_T(ID, W, BN_, C, KIND, M, SCHED, 0, NAME)
 
 static const Config kConfigs[] = {
     FA_CFG(0, 4, 64, 0, 0, 32, 0, "bm128_bn64_w4_m32_noncausal"),
@@ -257,6 +260,11 @@ static const Config kConfigs[] = {
     FA_CFG(13, 4, 64, 1, 1, 16, 0, "bm128_bn64_w4_m16_causal_splitkv"),
     FA_CFG(14, 8, 64, 0, 2, 16, 1, "bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
     FA_CFG(15, 8, 64, 1, 2, 16, 1, "bm256_bn64_w8_m16_pingpong_persistent_causal"),
+    // bf16 twins of the dispatched fp16 tiers
+    FA_CFG_T(16, 4, 64, 0, 0, 16, 0, 1, "bf16_bm128_bn64_w4_m16_noncausal"),
+    FA_CFG_T(17, 4, 64, 1, 0, 16, 0, 1, "bf16_bm128_bn64_w4_m16_causal"),
+    FA_CFG_T(18, 8, 64, 0, 2, 16, 1, 1, "bf16_bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
+    FA_CFG_T(19, 8, 64, 1, 2, 16, 1, 1, "bf16_bm256_bn64_w8_m16_pingpong_persistent_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -377,9 +385,49 @@ extern "C" int fa_fwd_f16_config(const void* q, const void* k, const void* v, vo
   if (rc != FA_OK) return rc;
   if (config_id < 0 || config_id >= kNumConfigs) return FA_ERR_BAD_CONFIG;
   const Config& cfg = kConfigs[config_id];
-  if (cfg.info.causal != (causal ? 1 : 0) || cfg.info.split_kv) return FA_ERR_BAD_CONFIG;
+  if (cfg.info.causal != (causal ? 1 : 0) || cfg.info.split_kv || cfg.info.dtype != FA_DTYPE_F16)
+    return FA_ERR_BAD_CONFIG;
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
   return launch(config_id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
+                (hipStream_t)hip_stream);
+}
+
+// the bf16 twin of an fp16 config (same tile shape, schedule and kind), or -1
+static int bf16_twin(int id) {
+  const Config& c = kConfigs[id];
+  for (int i = 0; i < kNumConfigs; ++i) {
+    const Config& t = kConfigs[i];
+    if (t.info.dtype == FA_DTYPE_BF16 && t.info.waves == c.info.waves &&
+        t.info.block_n == c.info.block_n && t.info.causal == c.info.causal &&
+        t.info.split_kv == c.info.split_kv && t.mfma == c.mfma && t.sched == c.sched &&
+        t.kind == c.kind)
+      return i;
+  }
+  return -1;
+}
+
+extern "C" int fa_fwd_bf16_config(const void* q, const void* k, const void* v, void* o,
+                                  int batch, int heads, int seq_len, int head_dim, int causal,
+                                  int config_id, void* hip_stream) {
+  int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
+  if (rc != FA_OK) return rc;
+  if (config_id < 0 || config_id >= kNumConfigs) return FA_ERR_BAD_CONFIG;
+  const Config& cfg = kConfigs[config_id];
+  if (cfg.info.causal != (causal ? 1 : 0) || cfg.info.split_kv || cfg.info.dtype != FA_DTYPE_BF16)
+    return FA_ERR_BAD_CONFIG;
+  if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
+  return launch(config_id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
+                (hipStream_t)hip_stream);
+}
+
+extern "C" int fa_fwd_bf16(const void* q, const void* k, const void* v, void* o, int batch,
+                           int heads, int seq_len, int head_dim, int causal, void* hip_stream) {
+  int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
+  if (rc != FA_OK) return rc;
+  if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
+  const int id = bf16_twin(fa_select_config(batch, heads, seq_len, causal));
+  if (id < 0) return FA_ERR_BAD_CONFIG;
+  return launch(id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
                 (hipStream_t)hip_stream);
 }
 

@@ -371,17 +371,35 @@ struct M32 {
 //    RESCALE_LOG2 (wave-uniform branch).
 // ---------------------------------------------------------------------------
 
-template <int BN_>
+// 16-bit element type of Q/K/V/O and of the MFMA operands: fp16 (the
+// reference's type) or bf16.  Storage, LDS images and transposed reads are
+// bit-identical for both; only the MFMA opcode and the fp32 <-> 16-bit
+// conversions differ.
+template <class T>
+struct Elem {
+  typedef T x8 __attribute__((ext_vector_type(8)));
+  typedef T x4 __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ f32x4 mfma(x8 a, x8 b, f32x4 c) {
+    if constexpr (std::is_same<T, __bf16>::value)
+      return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    else
+      return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+template <int BN_, class T = f16>
 struct M16 {
   static constexpr int BN = BN_;
   static constexpr int NKB = BN / 16;  // 16-key blocks per tile
   static constexpr int NU = BN / 32;   // 32-key PV steps per tile
+  typedef typename Elem<T>::x8 tx8;
+  typedef typename Elem<T>::x4 tx4;
   int lane, r16, g, sg;
   int kaddr[4], vaddr[2];
-  f16x8 qf[2][4];
+  tx8 qf[2][4];
   f32x4 acc[2][8];
   f32x4 s[2][NKB];
-  f16x8 pf[2][NU];
+  tx8 pf[2][NU];
   f32x4 negm[2];     // C operand of the QK^T chains: -m_ref broadcast
   float m_ref[2];    // reference max, log2 units (x = s*c - m_ref)
   f32x4 lacc[2];     // running row sums l (ones . P on the matrix pipe, in the PV chain)
@@ -418,7 +436,8 @@ struct M16 {
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int t = 0; t < 4; ++t)
-        qf[b][t] = buf_load16(rq, (qw + 16 * b + r16) * ROW_BYTES + (4 * t + g) * 16);
+        qf[b][t] = __builtin_bit_cast(
+            tx8, buf_load16(rq, (qw + 16 * b + r16) * ROW_BYTES + (4 * t + g) * 16));
   }
   __device__ __forceinline__ void scale_q() {
 #pragma unroll
@@ -426,7 +445,7 @@ struct M16 {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) qf[b][t][j] = (f16)((float)qf[b][t][j] * c);
+        for (int j = 0; j < 8; ++j) qf[b][t][j] = (T)((float)qf[b][t][j] * c);
   }
   __device__ __forceinline__ void load_q(__amdgpu_buffer_rsrc_t rq, int qw) {
     issue_q(rq, qw);
@@ -449,14 +468,13 @@ struct M16 {
 #pragma unroll
       for (int cb = 0; cb < NKB; ++cb) {
 #ifdef FA_DIAG_NO_LDS  // diagnostic timing build only: operands from registers
-        const f16x8 kf = qf[cb & 1][(t + cb) & 3];
+        const tx8 kf = qf[cb & 1][(t + cb) & 3];
 #else
-        const f16x8 kf = *reinterpret_cast<const f16x8*>(kb + kaddr[t] + 4096 * cb);
+        const tx8 kf = *reinterpret_cast<const tx8*>(kb + kaddr[t] + 4096 * cb);
 #endif
 #pragma unroll
         for (int b = 0; b < 2; ++b)
-          s[b][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[b][t], t == 0 ? negm[b] : s[b][cb],
-                                                            0, 0, 0);
+          s[b][cb] = Elem<T>::mfma(kf, qf[b][t], t == 0 ? negm[b] : s[b][cb]);
       }
   }
   // P = exp2(x) -> fp16, already in the B-operand layout of the PV product
@@ -472,7 +490,7 @@ struct M16 {
 #ifdef FA_ROWSUM_VALU
           lacc[b][0] += e;  // this lane's partial row sum (4 lanes per row)
 #endif
-          pf[b][cb >> 1][4 * (cb & 1) + i] = (f16)e;
+          pf[b][cb >> 1][4 * (cb & 1) + i] = (T)e;
         }
   }
   template <bool CAUSAL>
@@ -539,28 +557,28 @@ struct M16 {
     exp_p();
   }
   __device__ __forceinline__ void pv(const char* vb) {
-    const f16x8 ones = {(f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1};
+    const tx8 ones = {(T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f};
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
 #ifdef FA_DIAG_NO_LDS
-        const f16x8 vf = qf[e & 1][(u + e) & 3];
+        const tx8 vf = qf[e & 1][(u + e) & 3];
 #else
         const int base = 8192 * u + 512 * (e >> 1) + vaddr[e & 1];
-        const f16x4 lo = lds_read_tr(vb, base);
-        const f16x4 hi = lds_read_tr(vb, base + 4096);
-        const f16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        const tx4 lo = __builtin_bit_cast(tx4, lds_read_tr(vb, base));
+        const tx4 hi = __builtin_bit_cast(tx4, lds_read_tr(vb, base + 4096));
+        const tx8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 #endif
 #pragma unroll
         for (int b = 0; b < 2; ++b)
-          acc[b][e] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[b][u], acc[b][e], 0, 0, 0);
+          acc[b][e] = Elem<T>::mfma(vf, pf[b][u], acc[b][e]);
       }
       // row sums of the same fp16 P: every register of lacc[b] = l for q = lane&15
 #ifndef FA_ROWSUM_VALU
 #pragma unroll
       for (int b = 0; b < 2; ++b)
-        lacc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, pf[b][u], lacc[b], 0, 0, 0);
+        lacc[b] = Elem<T>::mfma(ones, pf[b][u], lacc[b]);
 #endif
     }
   }
@@ -627,10 +645,10 @@ struct M16 {
       const int rowb = (qw + 16 * b + r16) * ROW_BYTES;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        f16x4 w;
+        tx4 w;
 #pragma unroll
-        for (int x = 0; x < 4; ++x) w[x] = (f16)(acc[b][e][x] * inv);
-        buf_store8(ro, rowb + 2 * (16 * e + 4 * g), w);
+        for (int x = 0; x < 4; ++x) w[x] = (T)(acc[b][e][x] * inv);
+        buf_store8(ro, rowb + 2 * (16 * e + 4 * g), __builtin_bit_cast(f16x4, w));
       }
     }
   }

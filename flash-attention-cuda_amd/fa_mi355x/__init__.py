@@ -30,9 +30,14 @@ FA_ERR_HIP = 6
 FA_ERR_WORKSPACE = 7
 
 # every symbol include/fa_mi355x.h declares (tests check the .so exports them)
+FA_DTYPE_F16 = 0
+FA_DTYPE_BF16 = 1
+
 EXPORTED_SYMBOLS = (
     "fa_fwd_f16",
     "fa_fwd_f16_config",
+    "fa_fwd_bf16",
+    "fa_fwd_bf16_config",
     "fa_fwd_f16_splitkv",
     "fa_splitkv_num_splits",
     "fa_splitkv_o_bytes",
@@ -64,6 +69,7 @@ class _ConfigInfo(ctypes.Structure):
         ("split_kv", ctypes.c_int),
         ("lds_bytes", ctypes.c_int),
         ("name", ctypes.c_char_p),
+        ("dtype", ctypes.c_int),
     ]
 
 
@@ -87,6 +93,7 @@ class TileConfig:
     split_kv: bool
     lds_bytes: int
     name: str
+    dtype: str = "float16"  # element type of Q/K/V/O: "float16" or "bfloat16"
 
 
 _lib = None
@@ -113,6 +120,10 @@ def load_library() -> ctypes.CDLL:
     lib.fa_fwd_f16.restype = i
     lib.fa_fwd_f16_config.argtypes = [vp, vp, vp, vp, i, i, i, i, i, i, vp]
     lib.fa_fwd_f16_config.restype = i
+    lib.fa_fwd_bf16.argtypes = [vp, vp, vp, vp, i, i, i, i, i, vp]
+    lib.fa_fwd_bf16.restype = i
+    lib.fa_fwd_bf16_config.argtypes = [vp, vp, vp, vp, i, i, i, i, i, i, vp]
+    lib.fa_fwd_bf16_config.restype = i
     lib.fa_fwd_f16_splitkv.argtypes = [vp, vp, vp, vp, i, i, i, i, i, i, vp, vp, vp]
     lib.fa_fwd_f16_splitkv.restype = i
     lib.fa_splitkv_num_splits.argtypes = [i, i, i, i]
@@ -156,7 +167,8 @@ def configs() -> List[TileConfig]:
         _check(lib.fa_config_info(cid, ctypes.byref(ci)))
         out.append(
             TileConfig(ci.id, ci.block_m, ci.block_n, ci.waves, bool(ci.causal),
-                       bool(ci.split_kv), ci.lds_bytes, ci.name.decode())
+                       bool(ci.split_kv), ci.lds_bytes, ci.name.decode(),
+                       "bfloat16" if ci.dtype == FA_DTYPE_BF16 else "float16")
         )
     return out
 
@@ -184,9 +196,11 @@ def _stream_handle(stream) -> Optional[int]:
 def _check_qkvo(q, k, v, out):
     import torch
 
+    if q.dtype not in (torch.float16, torch.bfloat16):
+        raise FlashAttentionError(FA_ERR_BAD_SHAPE, f"q must be float16 or bfloat16, got {q.dtype}")
     for name, t in (("q", q), ("k", k), ("v", v), ("out", out)):
-        if t.dtype != torch.float16:
-            raise FlashAttentionError(FA_ERR_BAD_SHAPE, f"{name} must be float16, got {t.dtype}")
+        if t.dtype != q.dtype:
+            raise FlashAttentionError(FA_ERR_BAD_SHAPE, f"{name} must be {q.dtype}, got {t.dtype}")
         if not t.is_cuda:
             raise FlashAttentionError(FA_ERR_NULL_POINTER, f"{name} must be a device tensor")
         if not t.is_contiguous():
@@ -197,9 +211,10 @@ def _check_qkvo(q, k, v, out):
 
 def flash_attention_fwd(q, k, v, causal: bool = False, out=None, config: Optional[int] = None,
                         stream=None):
-    """O = softmax(Q K^T / sqrt(D) [+ causal mask]) V for fp16 BHSD tensors.
+    """O = softmax(Q K^T / sqrt(D) [+ causal mask]) V for fp16 or bf16 BHSD tensors.
 
-    q, k, v: [batch, heads, seq_len, 128] float16 contiguous device tensors.
+    q, k, v: [batch, heads, seq_len, 128] float16 (the reference's type) or
+    bfloat16 contiguous device tensors, all of one dtype.
     config: force a tile config id (see :func:`configs`); default = dispatcher.
     Enqueued on ``stream`` (default: torch's current stream); no sync.
     """
@@ -214,10 +229,11 @@ def flash_attention_fwd(q, k, v, causal: bool = False, out=None, config: Optiona
     args = (ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(k.data_ptr()),
             ctypes.c_void_p(v.data_ptr()), ctypes.c_void_p(out.data_ptr()), b, h, s, d,
             int(bool(causal)))
+    bf16 = q.dtype == torch.bfloat16
     if config is None:
-        _check(lib.fa_fwd_f16(*args, st))
+        _check((lib.fa_fwd_bf16 if bf16 else lib.fa_fwd_f16)(*args, st))
     else:
-        _check(lib.fa_fwd_f16_config(*args, int(config), st))
+        _check((lib.fa_fwd_bf16_config if bf16 else lib.fa_fwd_f16_config)(*args, int(config), st))
     return out
 
 

@@ -22,6 +22,7 @@ ap.add_argument("--causal", action="store_true")
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--iters", type=int, default=30)
 ap.add_argument("--env", default="", help="label only")
+ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"])
 ap.add_argument("--data", default="uniform", choices=["uniform", "zeros", "small"],
                 help="uniform[-0.5,0.5] (default), all zeros, or uniform[-0.01,0.01]")
 ap.add_argument("--libs", default="", help="comma list of library variants: '' = libfa_mi355x.so, "
@@ -30,7 +31,8 @@ a = ap.parse_args()
 g = torch.Generator(device="cuda")
 g.manual_seed(3)
 shape = (a.batch, a.heads, a.seq, 128)
-q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5, generator=g)
+dt = torch.bfloat16 if a.dtype == "bf16" else torch.float16
+q, k, v = (torch.empty(shape, dtype=dt, device="cuda").uniform_(-0.5, 0.5, generator=g)
            for _ in range(3))
 if a.data == "zeros":
     for t in (q, k, v):

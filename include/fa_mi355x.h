@@ -50,7 +50,10 @@ typedef struct {
   int split_kv;     /* 1 = writes fp32 partials for the LSE merge */
   int lds_bytes;    /* dynamic LDS per workgroup */
   const char* name;
+  int dtype;        /* FA_DTYPE_F16 or FA_DTYPE_BF16: element type of Q/K/V/O */
 } fa_config_info_t;
+
+enum { FA_DTYPE_F16 = 0, FA_DTYPE_BF16 = 1 };
 
 /* Per-config compiled resource usage: the reference's register/occupancy
  * report (cudaFuncGetAttributes + cudaOccupancyMaxActiveBlocksPerMultiprocessor,
@@ -77,6 +80,18 @@ int fa_fwd_f16(const void* q, const void* k, const void* v, void* o,
 int fa_fwd_f16_config(const void* q, const void* k, const void* v, void* o,
                       int batch, int heads, int seq_len, int head_dim,
                       int causal, int config_id, void* hip_stream);
+
+/* bf16 in/out (fp32 accumulate, P rounded to bf16 before PV): the same
+ * kernels on v_mfma_f32_16x16x32_bf16.  Not in the reference (fp16 only,
+ * :613); SURVEY.md §8(f) rank 4.  fa_fwd_bf16 uses the bf16 twin of
+ * fa_select_config()'s tier; fa_fwd_bf16_config accepts bf16 configs only
+ * (fa_config_info().dtype == FA_DTYPE_BF16), fa_fwd_f16_config fp16 only. */
+int fa_fwd_bf16(const void* q, const void* k, const void* v, void* o,
+                int batch, int heads, int seq_len, int head_dim, int causal,
+                void* hip_stream);
+int fa_fwd_bf16_config(const void* q, const void* k, const void* v, void* o,
+                       int batch, int heads, int seq_len, int head_dim,
+                       int causal, int config_id, void* hip_stream);
 
 /* Split-KV (flash-decoding) forward: the reference's dead IS_SPLITK path
  * (:169-180, :460-496) and its merge kernel flash_attention_splitk_merge

@@ -156,3 +156,27 @@ def test_python_mirror_rejects_bad_tensors():
     y = torch.zeros(1, 1, 8, 128, dtype=torch.float16)  # host tensor
     with pytest.raises(fa.FlashAttentionError):
         fa.flash_attention_fwd(y, y, y)
+
+
+def test_bf16_configs_and_entry_points():
+    """bf16 twins exist for the dispatched tiers; each entry point accepts
+    only its own dtype's configs (checked before any launch: no GPU needed)."""
+    fa = _fa()
+    lib = fa.load_library()
+    cfgs = fa.configs()
+    bf = [c for c in cfgs if c.dtype == "bfloat16"]
+    assert {c.causal for c in bf} == {False, True}
+    assert all(not c.split_kv for c in bf)
+    p = ctypes.c_void_p(0x1000)
+    f16_id = next(c.id for c in cfgs if c.dtype == "float16" and not c.causal and not c.split_kv)
+    bf_id = next(c.id for c in bf if not c.causal)
+    assert lib.fa_fwd_bf16_config(p, p, p, p, 1, 1, 64, 128, 0, f16_id, None) == fa.FA_ERR_BAD_CONFIG
+    assert lib.fa_fwd_f16_config(p, p, p, p, 1, 1, 64, 128, 0, bf_id, None) == fa.FA_ERR_BAD_CONFIG
+    assert lib.fa_fwd_bf16(p, p, p, p, 1, 1, 64, 64, 0, None) == fa.FA_ERR_UNSUPPORTED_HEAD_DIM
+    # the dispatcher's tier for each shape has a bf16 twin
+    for s in (64, 1024, 4096):
+        for b, h in ((1, 32), (64, 32)):
+            for causal in (False, True):
+                c = cfgs[fa.select_config(b, h, s, causal)]
+                assert any(t.waves == c.waves and t.causal == c.causal and t.block_m == c.block_m
+                           for t in bf), c.name
