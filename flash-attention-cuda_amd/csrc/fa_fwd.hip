@@ -68,12 +68,14 @@ __device__ __forceinline__ void map_block(int id, int nblk, int nqb, int bh_coun
 // SCHED: 0 = one-barrier-per-tile loop (any wave count), 1 = 8-wave ping-pong
 // (MFMA phase at s_setprio 1), 2 = ping-pong without the priority raise
 // BF16: Q/K/V/O and the MFMA operands are bf16 (16x16x32 policy only)
-template <int WAVES, int BN, bool CAUSAL, bool SPLIT, bool USE_M16, int SCHED, bool BF16 = false>
+// HDIM: head_dim (64 runs on the 16x16x32 policy only)
+template <int WAVES, int BN, bool CAUSAL, bool SPLIT, bool USE_M16, int SCHED, bool BF16 = false,
+          int HDIM = 128>
 __device__ __forceinline__ void run_tile_loop(const FwdParams& p, int bh, int qb, int split,
                                               char* smem) {
-  static_assert(USE_M16 || !BF16, "bf16 runs on the 16x16x32 policy");
-  using Pol = typename std::conditional<USE_M16, M16<BN, typename std::conditional<BF16, __bf16, f16>::type>,
-                                        M32<BN>>::type;
+  static_assert(USE_M16 || (!BF16 && HDIM == 128), "bf16 / head_dim 64 run on the 16x16x32 policy");
+  using Pol = typename std::conditional<
+      USE_M16, M16<BN, typename std::conditional<BF16, __bf16, f16>::type, HDIM>, M32<BN>>::type;
   if constexpr (SCHED == 1 || SCHED == 2) {
     static_assert(WAVES == 8, "ping-pong needs two groups of four waves");
     attention_pingpong<Pol, CAUSAL, SPLIT, SCHED == 1>(p, bh, qb, split, smem);
@@ -82,7 +84,8 @@ __device__ __forceinline__ void run_tile_loop(const FwdParams& p, int bh, int qb
   }
 }
 
-template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED, bool BF16 = false>
+template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED, bool BF16 = false,
+          int HDIM = 128>
 __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 #ifdef FA_STAMPS
@@ -91,7 +94,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_kernel(FwdParams p) 
 #endif
   int qb, bh;
   map_block(blockIdx.x, gridDim.x, p.nqb, p.bh, p.band, CAUSAL, qb, bh);
-  run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED, BF16>(p, bh, qb, 0, smem);
+  run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED, BF16, HDIM>(p, bh, qb, 0, smem);
 #ifdef FA_STAMPS
   if (threadIdx.x == 0 && blockIdx.x < FA_MAX_TIMELINE) {
     unsigned hw, xcc;
@@ -136,7 +139,8 @@ __device__ __forceinline__ void xcd_item(int j, int hx, int nqb, int band, bool 
   }
 }
 
-template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED, bool BF16 = false>
+template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED, bool BF16 = false,
+          int HDIM = 128>
 __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int x = blockIdx.x & 7, lcu = blockIdx.x >> 3, C = gridDim.x >> 3;
@@ -153,7 +157,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(Fw
       const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
       const unsigned long long c_start = __builtin_amdgcn_s_memtime();
 #endif
-      run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED, BF16>(p, bh, qb, 0, smem);
+      run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED, BF16, HDIM>(p, bh, qb, 0, smem);
 #ifdef FA_STAMPS
       const int rec = bh * p.nqb + qb;
       if (threadIdx.x == 0 && rec < FA_MAX_TIMELINE) {
@@ -226,21 +230,24 @@ struct Config {
   kernel_fn fn;
 };
 
-template <int W, int BN_, int C, int SPL, int M, int SCHED, int DT>
+template <int W, int BN_, int C, int SPL, int M, int SCHED, int DT, int HDIM>
 constexpr kernel_fn pick_kernel() {
   if constexpr (SPL == 1)
     return fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
   else if constexpr (SPL == 2)
-    return fa_fwd_f16_persistent_kernel<W, BN_, (C != 0), (M == 16), SCHED, DT == 1>;
+    return fa_fwd_f16_persistent_kernel<W, BN_, (C != 0), (M == 16), SCHED, DT == 1, HDIM>;
   else
-    return fa_fwd_f16_kernel<W, BN_, (C != 0), (M == 16), SCHED, DT == 1>;
+    return fa_fwd_f16_kernel<W, BN_, (C != 0), (M == 16), SCHED, DT == 1, HDIM>;
 }
 
 // KIND: 0 = one workgroup per (head, query block), 1 = split-KV, 2 = persistent
 // DT: 0 = fp16, 1 = bf16 (FA_DTYPE_*)
-#define FA_CFG_T(ID, W, BN_, C, KIND, M, SCHED, DT, NAME)                              \
-  {{ID, 32 * (W), BN_, W, C, (KIND) == 1, 4 * (BN_) * ROW_BYTES, NAME, DT}, M, SCHED, KIND, \
-   pick_kernel<W, BN_, C, KIND, M, SCHED, DT>()}
+// LDS images keep 256-B row slots at head_dim 64 too (fa_fwd_kernel.hpp M16)
+#define FA_CFG_TD(ID, W, BN_, C, KIND, M, SCHED, DT, HDIM, NAME)                           \
+  {{ID, 32 * (W), BN_, W, C, (KIND) == 1, 4 * (BN_) * ROW_BYTES, NAME, DT, HDIM}, M, SCHED, \
+   KIND, pick_kernel<W, BN_, C, KIND, M, SCHED, DT, HDIM>()}
+#define FA_CFG_T(ID, W, BN_, C, KIND, M, SCHED, DT, NAME) \
+  FA_CFG_TD(ID, W, BN_, C, KIND, M, SCHED, DT, 128, NAME)
 #define FA_CFG(ID, W, BN_, C, KIND, M, SCHED, NAME) FA_CFG_T(ID, W, BN_, C, KIND, M, SCHED, 0, NAME)
 
 static const Config kConfigs[] = {
@@ -265,6 +272,16 @@ static const Config kConfigs[] = {
     FA_CFG_T(17, 4, 64, 1, 0, 16, 0, 1, "bf16_bm128_bn64_w4_m16_causal"),
     FA_CFG_T(18, 8, 64, 0, 2, 16, 1, 1, "bf16_bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
     FA_CFG_T(19, 8, 64, 1, 2, 16, 1, 1, "bf16_bm256_bn64_w8_m16_pingpong_persistent_causal"),
+    // head_dim 64 twins (fp16, bf16)
+    FA_CFG_TD(20, 4, 64, 0, 0, 16, 0, 0, 64, "d64_bm128_bn64_w4_m16_noncausal"),
+    FA_CFG_TD(21, 4, 64, 1, 0, 16, 0, 0, 64, "d64_bm128_bn64_w4_m16_causal"),
+    FA_CFG_TD(22, 8, 64, 0, 2, 16, 1, 0, 64, "d64_bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
+    FA_CFG_TD(23, 8, 64, 1, 2, 16, 1, 0, 64, "d64_bm256_bn64_w8_m16_pingpong_persistent_causal"),
+    FA_CFG_TD(24, 4, 64, 0, 0, 16, 0, 1, 64, "bf16_d64_bm128_bn64_w4_m16_noncausal"),
+    FA_CFG_TD(25, 4, 64, 1, 0, 16, 0, 1, 64, "bf16_d64_bm128_bn64_w4_m16_causal"),
+    FA_CFG_TD(26, 8, 64, 0, 2, 16, 1, 1, 64,
+              "bf16_d64_bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
+    FA_CFG_TD(27, 8, 64, 1, 2, 16, 1, 1, 64, "bf16_d64_bm256_bn64_w8_m16_pingpong_persistent_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -309,7 +326,7 @@ static int num_cus() {
 static int check_args(const void* q, const void* k, const void* v, const void* o, int batch,
                       int heads, int seq_len, int head_dim) {
   if (batch < 0 || heads < 0 || seq_len < 0 || head_dim < 0) return FA_ERR_BAD_SHAPE;
-  if (head_dim != HD) return FA_ERR_UNSUPPORTED_HEAD_DIM;
+  if (head_dim != 128 && head_dim != 64) return FA_ERR_UNSUPPORTED_HEAD_DIM;
   if ((long long)batch * heads > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
   if (!q || !k || !v || !o) return FA_ERR_NULL_POINTER;
@@ -333,7 +350,7 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   p.bh = bh;
   p.nqb = (seq_len + cfg.info.block_m - 1) / cfg.info.block_m;
   p.num_splits = num_splits;
-  p.scale = 1.0f / sqrtf((float)HD);          // ref :612
+  p.scale = 1.0f / sqrtf((float)cfg.info.head_dim);  // ref :612
   p.c = p.scale * 1.4426950408889634f;        // LOG2E, ref :239
   // few heads per XCD: plain heaviest-first balances better; many: keep the
   // query blocks of a head together for L2 reuse (profiles/r01_band_ab.txt)
@@ -355,10 +372,48 @@ static int cfg_for(int waves, int bn, int causal, int mfma, int sched, int kind 
   for (int i = 0; i < kNumConfigs; ++i)
     if (kConfigs[i].info.waves == waves && kConfigs[i].info.block_n == bn &&
         kConfigs[i].info.causal == causal && kConfigs[i].kind == kind &&
-        kConfigs[i].mfma == mfma && kConfigs[i].sched == sched)
+        kConfigs[i].mfma == mfma && kConfigs[i].sched == sched &&
+        kConfigs[i].info.dtype == FA_DTYPE_F16 && kConfigs[i].info.head_dim == 128)
       return i;
   return -1;
 }
+
+// the twin of a config for another element type / head_dim (same tile
+// shape, schedule and kind), or -1
+static int twin(int id, int dtype, int head_dim) {
+  if (id < 0) return -1;
+  const Config& c = kConfigs[id];
+  for (int i = 0; i < kNumConfigs; ++i) {
+    const Config& t = kConfigs[i];
+    if (t.info.dtype == dtype && t.info.head_dim == head_dim && t.info.waves == c.info.waves &&
+        t.info.block_n == c.info.block_n && t.info.causal == c.info.causal &&
+        t.info.split_kv == c.info.split_kv && t.mfma == c.mfma && t.sched == c.sched &&
+        t.kind == c.kind)
+      return i;
+  }
+  return -1;
+}
+
+// one forced config: its mask, dtype and head_dim must match the call
+static int launch_config(int config_id, int dtype, const void* q, const void* k, const void* v,
+                         void* o, int batch, int heads, int seq_len, int head_dim, int causal,
+                         void* hip_stream) {
+  int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
+  if (rc != FA_OK) return rc;
+  if (config_id < 0 || config_id >= kNumConfigs) return FA_ERR_BAD_CONFIG;
+  const Config& cfg = kConfigs[config_id];
+  if (cfg.info.causal != (causal ? 1 : 0) || cfg.info.split_kv || cfg.info.dtype != dtype)
+    return FA_ERR_BAD_CONFIG;
+  if (cfg.info.head_dim != head_dim) return FA_ERR_UNSUPPORTED_HEAD_DIM;
+  if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
+  return launch(config_id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
+                (hipStream_t)hip_stream);
+}
+
+// dispatcher tier, as the twin for this dtype / head_dim
+static int launch_auto(int dtype, const void* q, const void* k, const void* v, void* o,
+                       int batch, int heads, int seq_len, int head_dim, int causal,
+                       void* hip_stream);
 
 }  // namespace fa
 
@@ -378,67 +433,44 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
 }
 
+namespace fa {
+static int launch_auto(int dtype, const void* q, const void* k, const void* v, void* o,
+                           int batch, int heads, int seq_len, int head_dim, int causal,
+                           void* hip_stream) {
+  int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
+  if (rc != FA_OK) return rc;
+  if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
+  const int id = twin(fa_select_config(batch, heads, seq_len, causal), dtype, head_dim);
+  if (id < 0) return FA_ERR_BAD_CONFIG;
+  return launch(id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
+                (hipStream_t)hip_stream);
+}
+}  // namespace fa
+
 extern "C" int fa_fwd_f16_config(const void* q, const void* k, const void* v, void* o,
                                  int batch, int heads, int seq_len, int head_dim, int causal,
                                  int config_id, void* hip_stream) {
-  int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
-  if (rc != FA_OK) return rc;
-  if (config_id < 0 || config_id >= kNumConfigs) return FA_ERR_BAD_CONFIG;
-  const Config& cfg = kConfigs[config_id];
-  if (cfg.info.causal != (causal ? 1 : 0) || cfg.info.split_kv || cfg.info.dtype != FA_DTYPE_F16)
-    return FA_ERR_BAD_CONFIG;
-  if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
-  return launch(config_id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
-                (hipStream_t)hip_stream);
-}
-
-// the bf16 twin of an fp16 config (same tile shape, schedule and kind), or -1
-static int bf16_twin(int id) {
-  const Config& c = kConfigs[id];
-  for (int i = 0; i < kNumConfigs; ++i) {
-    const Config& t = kConfigs[i];
-    if (t.info.dtype == FA_DTYPE_BF16 && t.info.waves == c.info.waves &&
-        t.info.block_n == c.info.block_n && t.info.causal == c.info.causal &&
-        t.info.split_kv == c.info.split_kv && t.mfma == c.mfma && t.sched == c.sched &&
-        t.kind == c.kind)
-      return i;
-  }
-  return -1;
+  return launch_config(config_id, FA_DTYPE_F16, q, k, v, o, batch, heads, seq_len, head_dim,
+                       causal, hip_stream);
 }
 
 extern "C" int fa_fwd_bf16_config(const void* q, const void* k, const void* v, void* o,
                                   int batch, int heads, int seq_len, int head_dim, int causal,
                                   int config_id, void* hip_stream) {
-  int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
-  if (rc != FA_OK) return rc;
-  if (config_id < 0 || config_id >= kNumConfigs) return FA_ERR_BAD_CONFIG;
-  const Config& cfg = kConfigs[config_id];
-  if (cfg.info.causal != (causal ? 1 : 0) || cfg.info.split_kv || cfg.info.dtype != FA_DTYPE_BF16)
-    return FA_ERR_BAD_CONFIG;
-  if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
-  return launch(config_id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
-                (hipStream_t)hip_stream);
+  return launch_config(config_id, FA_DTYPE_BF16, q, k, v, o, batch, heads, seq_len, head_dim,
+                       causal, hip_stream);
 }
 
 extern "C" int fa_fwd_bf16(const void* q, const void* k, const void* v, void* o, int batch,
                            int heads, int seq_len, int head_dim, int causal, void* hip_stream) {
-  int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
-  if (rc != FA_OK) return rc;
-  if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
-  const int id = bf16_twin(fa_select_config(batch, heads, seq_len, causal));
-  if (id < 0) return FA_ERR_BAD_CONFIG;
-  return launch(id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
-                (hipStream_t)hip_stream);
+  return launch_auto(FA_DTYPE_BF16, q, k, v, o, batch, heads, seq_len, head_dim, causal,
+                     hip_stream);
 }
 
 extern "C" int fa_fwd_f16(const void* q, const void* k, const void* v, void* o, int batch,
                           int heads, int seq_len, int head_dim, int causal, void* hip_stream) {
-  int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
-  if (rc != FA_OK) return rc;
-  if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
-  const int id = fa_select_config(batch, heads, seq_len, causal);
-  return launch(id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
-                (hipStream_t)hip_stream);
+  return launch_auto(FA_DTYPE_F16, q, k, v, o, batch, heads, seq_len, head_dim, causal,
+                     hip_stream);
 }
 
 // ---- split-KV ---------------------------------------------------------------
@@ -474,6 +506,7 @@ extern "C" int fa_fwd_f16_splitkv(const void* q, const void* k, const void* v, v
                                   int batch, int heads, int seq_len, int head_dim, int causal,
                                   int num_splits, float* part_o, float* part_ml,
                                   void* hip_stream) {
+  if (head_dim != HD) return FA_ERR_UNSUPPORTED_HEAD_DIM;  // split-KV: head_dim 128 only
   int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
   if (rc != FA_OK) return rc;
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;

@@ -153,6 +153,8 @@ __device__ unsigned long long g_fa_timeline[FA_MAX_TIMELINE][4];  // + shader cy
 template <int BN_>
 struct M32 {
   static constexpr int BN = BN_;
+  static constexpr int HDIM = 128;  // head_dim 128 only
+  static constexpr int RPW = 4;     // tile rows one wave stages per pass
   static constexpr int NSB = BN / 32;  // 32-key S^T blocks per tile
   int lane, r, h;
   int kaddr0, kaddr1, vaddr0, vaddr1;
@@ -387,17 +389,26 @@ struct Elem {
   }
 };
 
-template <int BN_, class T = f16>
+template <int BN_, class T = f16, int HDIM_ = 128>
 struct M16 {
+  static_assert(HDIM_ == 64 || HDIM_ == 128, "head_dim 64 or 128");
   static constexpr int BN = BN_;
+  static constexpr int HDIM = HDIM_;      // head_dim
+  static constexpr int ROW = 2 * HDIM;    // bytes per Q/K/V/O row in HBM
+  static constexpr int NTQ = HDIM / 32;   // 32-wide k-steps of QK^T (Q fragments per 16 rows)
+  static constexpr int NE = HDIM / 16;    // 16-wide d-blocks of O
+  static constexpr int RPW = 512 / HDIM;  // tile rows one wave stages per pass (64 lanes x 16 B)
+  // LDS images keep 256-B row slots at either head_dim (a 64-wide row uses
+  // half of each slot), so every address formula and its bank analysis is
+  // the head_dim-128 one.
   static constexpr int NKB = BN / 16;  // 16-key blocks per tile
   static constexpr int NU = BN / 32;   // 32-key PV steps per tile
   typedef typename Elem<T>::x8 tx8;
   typedef typename Elem<T>::x4 tx4;
   int lane, r16, g, sg;
   int kaddr[4], vaddr[2];
-  tx8 qf[2][4];
-  f32x4 acc[2][8];
+  tx8 qf[2][NTQ];
+  f32x4 acc[2][NE];
   f32x4 s[2][NKB];
   tx8 pf[2][NU];
   f32x4 negm[2];     // C operand of the QK^T chains: -m_ref broadcast
@@ -414,7 +425,7 @@ struct M16 {
     sg = ((g & 1) << 1) | (g >> 1);
     const int krow = 4 * ((((r16 >> 2) & 1) << 1) | (r16 >> 3)) + (r16 & 3);  // sigma(r16)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) kaddr[t] = k_off16(krow, 4 * t + g);
+    for (int t = 0; t < 4; ++t) kaddr[t] = k_off16(krow, 4 * t + g);  // t < NTQ used
     const int i = lane & 15, qq = i >> 2, pp = i & 3;
 #pragma unroll
     for (int ep = 0; ep < 2; ++ep)
@@ -423,7 +434,7 @@ struct M16 {
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[b][e] = f32x4{};
+      for (int e = 0; e < NE; ++e) acc[b][e] = f32x4{};
       negm[b] = f32x4{};
       m_ref[b] = 0.f;
       lacc[b] = f32x4{};
@@ -435,15 +446,15 @@ struct M16 {
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < NTQ; ++t)
         qf[b][t] = __builtin_bit_cast(
-            tx8, buf_load16(rq, (qw + 16 * b + r16) * ROW_BYTES + (4 * t + g) * 16));
+            tx8, buf_load16(rq, (qw + 16 * b + r16) * ROW + (4 * t + g) * 16));
   }
   __device__ __forceinline__ void scale_q() {
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < NTQ; ++t)
 #pragma unroll
         for (int j = 0; j < 8; ++j) qf[b][t][j] = (T)((float)qf[b][t][j] * c);
   }
@@ -452,23 +463,30 @@ struct M16 {
     scale_q();
   }
   // K staging: natural row-major lanes (8 lanes = 8 chunks of one row: conflict-free
-  // writes into image B); V staging as M32 (image A)
-  __device__ __forceinline__ int k_stage_row(int wave) const { return 4 * wave + (lane >> 4); }
-  __device__ __forceinline__ int k_stage_ch() const { return lane & 15; }
-  __device__ __forceinline__ int v_stage_row(int wave) const {
-    return 4 * wave + 2 * ((lane >> 5) & 1) + ((lane >> 2) & 1);
+  // writes into image B); V staging: each group of 8 lanes = two rows of opposite
+  // parity x 4 chunks (conflict-free writes into image A).  A wave stages RPW rows
+  // per pass: 4 rows x 16 chunks (head_dim 128) or 8 rows x 8 chunks (64).
+  __device__ __forceinline__ int k_stage_row(int wave) const {
+    return HDIM == 128 ? 4 * wave + (lane >> 4) : 8 * wave + (lane >> 3);
   }
-  __device__ __forceinline__ int v_stage_ch() const { return 4 * ((lane >> 3) & 3) + (lane & 3); }
+  __device__ __forceinline__ int k_stage_ch() const { return HDIM == 128 ? lane & 15 : lane & 7; }
+  __device__ __forceinline__ int v_stage_row(int wave) const {
+    return HDIM == 128 ? 4 * wave + 2 * ((lane >> 5) & 1) + ((lane >> 2) & 1)
+                       : 8 * wave + 2 * ((lane >> 4) & 3) + ((lane >> 2) & 1);
+  }
+  __device__ __forceinline__ int v_stage_ch() const {
+    return HDIM == 128 ? 4 * ((lane >> 3) & 3) + (lane & 3) : 4 * ((lane >> 3) & 1) + (lane & 3);
+  }
   static __device__ __forceinline__ int k_lds(int row, int ch) { return k_off16(row, ch); }
   static __device__ __forceinline__ int v_lds(int row, int ch) { return lds_off(row, ch); }
 
   __device__ __forceinline__ void qk(const char* kb) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < NTQ; ++t)
 #pragma unroll
       for (int cb = 0; cb < NKB; ++cb) {
 #ifdef FA_DIAG_NO_LDS  // diagnostic timing build only: operands from registers
-        const tx8 kf = qf[cb & 1][(t + cb) & 3];
+        const tx8 kf = qf[cb & 1][(t + cb) & (NTQ - 1)];
 #else
         const tx8 kf = *reinterpret_cast<const tx8*>(kb + kaddr[t] + 4096 * cb);
 #endif
@@ -544,7 +562,7 @@ struct M16 {
         if (have_ref) {
           const float alpha = __builtin_amdgcn_exp2f(-sh);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) acc[b][e] *= alpha;
+          for (int e = 0; e < NE; ++e) acc[b][e] *= alpha;
           lacc[b] *= alpha;
         }
 #pragma unroll
@@ -561,9 +579,9 @@ struct M16 {
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < NE; ++e) {
 #ifdef FA_DIAG_NO_LDS
-        const tx8 vf = qf[e & 1][(u + e) & 3];
+        const tx8 vf = qf[e & 1][(u + e) & (NTQ - 1)];
 #else
         const int base = 8192 * u + 512 * (e >> 1) + vaddr[e & 1];
         const tx4 lo = __builtin_bit_cast(tx4, lds_read_tr(vb, base));
@@ -595,22 +613,25 @@ struct M16 {
     if (do_pv) {
       pv(vb);
 #if FA_PV_PIPE > 0
-      __builtin_amdgcn_sched_group_barrier(0x100, FA_PV_PIPE, 0);
+      constexpr int PV_READS = 2 * NE * NU, PV_MFMAS = 2 * NE * NU + 2 * NU;
+      constexpr int PV_AHEAD = FA_PV_PIPE < PV_READS ? FA_PV_PIPE : PV_READS;
+      __builtin_amdgcn_sched_group_barrier(0x100, PV_AHEAD, 0);
 #pragma unroll
-      for (int i = 0; i < (32 - FA_PV_PIPE) / 2; ++i) {
+      for (int i = 0; i < (PV_READS - PV_AHEAD) / 2; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, 36, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, PV_MFMAS, 0);
 #endif
     }
     __builtin_amdgcn_sched_barrier(0);
     if (do_qk) {
       qk(kb);
       // keep FA_QK_PIPE K reads in flight ahead of the MFMAs that consume them
+      constexpr int QK_READS = NTQ * NKB;
       __builtin_amdgcn_sched_group_barrier(0x100, FA_QK_PIPE, 0);
 #pragma unroll
-      for (int i = 0; i < 16 - FA_QK_PIPE; ++i) {
+      for (int i = 0; i < QK_READS - FA_QK_PIPE; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
@@ -642,9 +663,9 @@ struct M16 {
     for (int b = 0; b < 2; ++b) {
       const float lt = row_sum(b);  // already the full row sum (MFMA over all keys)
       const float inv = lt > 0.f ? 1.0f / lt : 0.f;
-      const int rowb = (qw + 16 * b + r16) * ROW_BYTES;
+      const int rowb = (qw + 16 * b + r16) * ROW;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < NE; ++e) {
         tx4 w;
 #pragma unroll
         for (int x = 0; x < 4; ++x) w[x] = (T)(acc[b][e][x] * inv);
@@ -660,7 +681,7 @@ struct M16 {
       const float lt = row_sum(b);
       const int q = qw + 16 * b + r16;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) buf_store16f(rpo, q * HD * 4 + 4 * (16 * e + 4 * g), acc[b][e]);
+      for (int e = 0; e < NE; ++e) buf_store16f(rpo, q * HDIM * 4 + 4 * (16 * e + 4 * g), acc[b][e]);
       if (g == 0 && q < S)
         *reinterpret_cast<float2*>(pml + (size_t)q * 2) =
             make_float2(lt > 0.f ? m_ref[b] * 0.6931471805599453f : ninf(), lt);
@@ -681,9 +702,11 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
   constexpr int BN = Pol::BN;
   constexpr int NT = WAVES * 64;
   constexpr int BM = WAVES * 32;
-  constexpr int TILE_BYTES = BN * ROW_BYTES;
-  constexpr int NCH = (BN * 16) / NT;  // 16-B chunks per thread per tile (K and V each)
-  static_assert((BN * 16) % NT == 0, "tile chunks must divide evenly");
+  constexpr int HD = Pol::HDIM;            // shadows the head_dim-128 defaults
+  constexpr int ROW_BYTES = 2 * HD;        // HBM row
+  constexpr int TILE_BYTES = BN * 256;     // LDS image: 256-B row slots at any head_dim
+  constexpr int NCH = (BN * (HD / 8)) / NT;  // 16-B chunks per thread per tile (K and V each)
+  static_assert((BN * (HD / 8)) % NT == 0, "tile chunks must divide evenly");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -722,16 +745,16 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
     const auto rv = make_rsrc(Vh + (size_t)kv_base * HD, bytes);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      kst[i] = buf_load16(rk, (kr0 + 4 * WAVES * i) * ROW_BYTES + kc * 16);
-      vst[i] = buf_load16(rv, (vr0 + 4 * WAVES * i) * ROW_BYTES + vc * 16);
+      kst[i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
+      vst[i] = buf_load16(rv, (vr0 + Pol::RPW * WAVES * i) * ROW_BYTES + vc * 16);
     }
   };
   auto write_lds = [&](char* kb) {
     char* vb = kb + TILE_BYTES;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      *reinterpret_cast<f16x8*>(kb + Pol::k_lds(kr0 + 4 * WAVES * i, kc)) = kst[i];
-      *reinterpret_cast<f16x8*>(vb + Pol::v_lds(vr0 + 4 * WAVES * i, vc)) = vst[i];
+      *reinterpret_cast<f16x8*>(kb + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = kst[i];
+      *reinterpret_cast<f16x8*>(vb + Pol::v_lds(vr0 + Pol::RPW * WAVES * i, vc)) = vst[i];
     }
   };
 
@@ -800,9 +823,11 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   constexpr int BN = Pol::BN;
   constexpr int NT = WAVES * 64;
   constexpr int BM = WAVES * 32;
-  constexpr int TILE_BYTES = BN * ROW_BYTES;
-  constexpr int NCH = (BN * 16) / NT;
-  static_assert((BN * 16) % NT == 0, "tile chunks must divide evenly");
+  constexpr int HD = Pol::HDIM;            // shadows the head_dim-128 defaults
+  constexpr int ROW_BYTES = 2 * HD;        // HBM row
+  constexpr int TILE_BYTES = BN * 256;     // LDS image: 256-B row slots at any head_dim
+  constexpr int NCH = (BN * (HD / 8)) / NT;
+  static_assert((BN * (HD / 8)) % NT == 0, "tile chunks must divide evenly");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -851,8 +876,8 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     const auto rv = make_rsrc(Vh + (size_t)vb_row * HD, (kv_hi - vb_row) * ROW_BYTES);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      kst[i] = buf_load16(rk, (kr0 + 4 * WAVES * i) * ROW_BYTES + kc * 16);
-      vst[i] = buf_load16(rv, (vr0 + 4 * WAVES * i) * ROW_BYTES + vc * 16);
+      kst[i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
+      vst[i] = buf_load16(rv, (vr0 + Pol::RPW * WAVES * i) * ROW_BYTES + vc * 16);
     }
   };
   auto write_tile = [&](int k) {
@@ -860,8 +885,8 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     char* vb = vbuf0 + (k & 1) * TILE_BYTES;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      *reinterpret_cast<f16x8*>(kb + Pol::k_lds(kr0 + 4 * WAVES * i, kc)) = kst[i];
-      *reinterpret_cast<f16x8*>(vb + Pol::v_lds(vr0 + 4 * WAVES * i, vc)) = vst[i];
+      *reinterpret_cast<f16x8*>(kb + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = kst[i];
+      *reinterpret_cast<f16x8*>(vb + Pol::v_lds(vr0 + Pol::RPW * WAVES * i, vc)) = vst[i];
     }
   };
 
@@ -872,12 +897,12 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     f16x8 k0[NCH];
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
-      k0[i] = buf_load16(rk, (kr0 + 4 * WAVES * i) * ROW_BYTES + kc * 16);
+      k0[i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
     if ((kIssueInSm || grp == 1) && n > 0) issue_tile(0);
     pol.scale_q();
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
-      *reinterpret_cast<f16x8*>(kbuf0 + Pol::k_lds(kr0 + 4 * WAVES * i, kc)) = k0[i];
+      *reinterpret_cast<f16x8*>(kbuf0 + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = k0[i];
   }
   // Q and K_0 retired before the loop (see attention_tile_loop); group B's
   // tile-0 loads may stay in flight (they are the 2*NCH most recent)
@@ -915,7 +940,7 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     __syncthreads();
   }
 #ifdef FA_STAMPS
-  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 1}, st0, st01, st1, st2, st3, st4;
+  unsigned long long st_acc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0}, st0, st01, st1, st2, st3, st4;
   st_acc[7] = __builtin_amdgcn_s_memtime() - t_in;
 #define FA_STAMP(v)                                                                   \
   do {                                                                                \
@@ -943,6 +968,12 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
 #ifdef FA_STAMPS
     unsigned long long st25;
     FA_STAMP(st25);
+#endif
+#ifdef FA_STAMPS
+    unsigned long long st_w;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // diagnostic: split the load wait from the LDS writes
+    FA_STAMP(st_w);
+    st_acc[10] += st_w - st25;
 #endif
     if (t < n) write_tile(t);
     if (kIssueInSm && t + 1 < n) issue_tile(t + 1);
@@ -975,7 +1006,7 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   __builtin_amdgcn_s_waitcnt(0);  // stores issued and retired
   st_acc[8] = __builtin_amdgcn_s_memtime() - t_le;
   if (lane == 0 && blockIdx.x < 64)
-    for (int i = 0; i < 10; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
+    for (int i = 0; i < 11; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
 #endif
 #undef FA_STAMP
 }

@@ -70,6 +70,7 @@ class _ConfigInfo(ctypes.Structure):
         ("lds_bytes", ctypes.c_int),
         ("name", ctypes.c_char_p),
         ("dtype", ctypes.c_int),
+        ("head_dim", ctypes.c_int),
     ]
 
 
@@ -94,6 +95,7 @@ class TileConfig:
     lds_bytes: int
     name: str
     dtype: str = "float16"  # element type of Q/K/V/O: "float16" or "bfloat16"
+    head_dim: int = 128
 
 
 _lib = None
@@ -168,7 +170,7 @@ def configs() -> List[TileConfig]:
         out.append(
             TileConfig(ci.id, ci.block_m, ci.block_n, ci.waves, bool(ci.causal),
                        bool(ci.split_kv), ci.lds_bytes, ci.name.decode(),
-                       "bfloat16" if ci.dtype == FA_DTYPE_BF16 else "float16")
+                       "bfloat16" if ci.dtype == FA_DTYPE_BF16 else "float16", ci.head_dim)
         )
     return out
 
@@ -213,8 +215,9 @@ def flash_attention_fwd(q, k, v, causal: bool = False, out=None, config: Optiona
                         stream=None):
     """O = softmax(Q K^T / sqrt(D) [+ causal mask]) V for fp16 or bf16 BHSD tensors.
 
-    q, k, v: [batch, heads, seq_len, 128] float16 (the reference's type) or
-    bfloat16 contiguous device tensors, all of one dtype.
+    q, k, v: [batch, heads, seq_len, D] float16 (the reference's type) or
+    bfloat16 contiguous device tensors, all of one dtype; D = 128 (the
+    reference's head_dim) or 64.
     config: force a tile config id (see :func:`configs`); default = dispatcher.
     Enqueued on ``stream`` (default: torch's current stream); no sync.
     """

@@ -20,6 +20,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--seqs", default="512,1024,2048,4096,8192,16384")
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--no-headline", action="store_true")
+ap.add_argument("--head-dim", type=int, default=128, choices=[64, 128])
+ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"])
 a = ap.parse_args()
 
 
@@ -47,12 +49,14 @@ def sdpa_backend_name():
 def run(b, h, s, causal):
     g = torch.Generator(device="cuda")
     g.manual_seed(42)
-    q, k, v = (torch.empty((b, h, s, 128), dtype=torch.float16, device="cuda")
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float16
+    q, k, v = (torch.empty((b, h, s, a.head_dim), dtype=dt, device="cuda")
                .uniform_(-0.5, 0.5, generator=g) for _ in range(3))
-    flops = fa.attention_flops(b, h, s, 128, causal)
+    flops = fa.attention_flops(b, h, s, a.head_dim, causal)
     iters = max(3, min(a.iters, int(2e13 / flops)))
     ours = torch.ops.fa_mi355x.fwd(q, k, v, causal)
-    row = {"batch": b, "heads": h, "seq": s, "causal": causal}
+    row = {"batch": b, "heads": h, "seq": s, "head_dim": a.head_dim, "dtype": a.dtype,
+           "causal": causal}
     ms = timed(lambda: torch.ops.fa_mi355x.fwd(q, k, v, causal), iters)
     row["fa_mi355x_tflops"] = round(flops / ms / 1e9, 1)
     try:

@@ -51,6 +51,7 @@ typedef struct {
   int lds_bytes;    /* dynamic LDS per workgroup */
   const char* name;
   int dtype;        /* FA_DTYPE_F16 or FA_DTYPE_BF16: element type of Q/K/V/O */
+  int head_dim;     /* 128 (the reference's) or 64 */
 } fa_config_info_t;
 
 enum { FA_DTYPE_F16 = 0, FA_DTYPE_BF16 = 1 };

@@ -40,7 +40,8 @@ def _ref(q, k, v, causal):
 
 
 def _bf16_configs(causal):
-    return [c.id for c in _fa().configs() if c.dtype == "bfloat16" and c.causal == causal]
+    return [c.id for c in _fa().configs()
+            if c.dtype == "bfloat16" and c.causal == causal and c.head_dim == 128]
 
 
 @pytest.mark.parametrize("causal", [False, True])

@@ -65,6 +65,7 @@ def test_config_table():
     cfgs = fa.configs()
     assert [c.id for c in cfgs] == list(range(len(cfgs)))
     for c in cfgs:
+        assert c.head_dim in (64, 128) and c.dtype in ("float16", "bfloat16")
         assert c.block_m == 32 * c.waves
         assert c.block_n % 32 == 0
         assert c.lds_bytes == 4 * c.block_n * 256 <= 160 * 1024
@@ -93,8 +94,9 @@ def _null_call(lib, head_dim=128, b=1, h=1, s=64, causal=0, ptr=None):
 def test_argument_errors_without_gpu():
     fa = _fa()
     lib = fa.load_library()
-    assert _null_call(lib, head_dim=64) == fa.FA_ERR_UNSUPPORTED_HEAD_DIM
+    assert _null_call(lib, head_dim=96) == fa.FA_ERR_UNSUPPORTED_HEAD_DIM
     assert _null_call(lib, head_dim=256) == fa.FA_ERR_UNSUPPORTED_HEAD_DIM
+    assert _null_call(lib, head_dim=64) == fa.FA_ERR_NULL_POINTER  # 64 is supported
     assert _null_call(lib, b=-1) == fa.FA_ERR_BAD_SHAPE
     assert _null_call(lib, s=-5) == fa.FA_ERR_BAD_SHAPE
     assert _null_call(lib) == fa.FA_ERR_NULL_POINTER
@@ -172,7 +174,11 @@ def test_bf16_configs_and_entry_points():
     bf_id = next(c.id for c in bf if not c.causal)
     assert lib.fa_fwd_bf16_config(p, p, p, p, 1, 1, 64, 128, 0, f16_id, None) == fa.FA_ERR_BAD_CONFIG
     assert lib.fa_fwd_f16_config(p, p, p, p, 1, 1, 64, 128, 0, bf_id, None) == fa.FA_ERR_BAD_CONFIG
-    assert lib.fa_fwd_bf16(p, p, p, p, 1, 1, 64, 64, 0, None) == fa.FA_ERR_UNSUPPORTED_HEAD_DIM
+    assert lib.fa_fwd_bf16(p, p, p, p, 1, 1, 64, 96, 0, None) == fa.FA_ERR_UNSUPPORTED_HEAD_DIM
+    # a forced config must match the call's head_dim
+    d64 = next(c.id for c in cfgs if c.head_dim == 64 and c.dtype == "float16" and not c.causal)
+    assert lib.fa_fwd_f16_config(p, p, p, p, 1, 1, 64, 128, 0, d64, None) == \
+        fa.FA_ERR_UNSUPPORTED_HEAD_DIM
     # the dispatcher's tier for each shape has a bf16 twin
     for s in (64, 1024, 4096):
         for b, h in ((1, 32), (64, 32)):

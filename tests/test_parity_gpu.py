@@ -75,7 +75,8 @@ def test_reference_checks(s, h, causal):
 def _configs(causal, split=False):
     fa = _fa()
     return [c.id for c in fa.configs()
-            if c.causal == causal and c.split_kv == split and c.dtype == "float16"]
+            if c.causal == causal and c.split_kv == split and c.dtype == "float16"
+            and c.head_dim == 128]
 
 
 @pytest.mark.parametrize("causal", [False, True])
@@ -140,7 +141,7 @@ def test_reference_signature_wrapper():
 
 def test_error_codes():
     fa = _fa()
-    q = torch.zeros(1, 1, 64, 64, dtype=torch.float16, device="cuda")
+    q = torch.zeros(1, 1, 64, 96, dtype=torch.float16, device="cuda")  # head_dim 64/128 only
     with pytest.raises(fa.FlashAttentionError) as e:
-        fa.flash_attention_v9_dispatch(q, q, q, q, None, None, 1, 1, 64, 64, False)
+        fa.flash_attention_v9_dispatch(q, q, q, q, None, None, 1, 1, 64, 96, False)
     assert e.value.status == fa.FA_ERR_UNSUPPORTED_HEAD_DIM

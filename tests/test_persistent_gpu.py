@@ -41,7 +41,7 @@ def _ids(kind_name):
     fa = _fa()
     out = {}
     for c in fa.configs():
-        if kind_name in c.name and c.dtype == "float16":
+        if kind_name in c.name and c.dtype == "float16" and c.head_dim == 128:
             out[c.causal] = c.id
     return out
 
