@@ -66,7 +66,8 @@ __device__ __forceinline__ void map_block(int id, int nblk, int nqb, int bh_coun
 }
 
 // SCHED: 0 = one-barrier-per-tile loop (any wave count), 1 = 8-wave ping-pong
-// (MFMA phase at s_setprio 1), 2 = ping-pong without the priority raise
+// (MFMA phase at s_setprio 1), 2 = ping-pong without the priority raise,
+// 3 = ping-pong with LDS-DMA tile loads into three rotating buffers
 // BF16: Q/K/V/O and the MFMA operands are bf16 (16x16x32 policy only)
 // HDIM: head_dim (64 runs on the 16x16x32 policy only)
 template <int WAVES, int BN, bool CAUSAL, bool SPLIT, bool USE_M16, int SCHED, bool BF16 = false,
@@ -76,9 +77,9 @@ __device__ __forceinline__ void run_tile_loop(const FwdParams& p, int bh, int qb
   static_assert(USE_M16 || (!BF16 && HDIM == 128), "bf16 / head_dim 64 run on the 16x16x32 policy");
   using Pol = typename std::conditional<
       USE_M16, M16<BN, typename std::conditional<BF16, __bf16, f16>::type, HDIM>, M32<BN>>::type;
-  if constexpr (SCHED == 1 || SCHED == 2) {
+  if constexpr (SCHED == 1 || SCHED == 2 || SCHED == 3) {
     static_assert(WAVES == 8, "ping-pong needs two groups of four waves");
-    attention_pingpong<Pol, CAUSAL, SPLIT, SCHED == 1>(p, bh, qb, split, smem);
+    attention_pingpong<Pol, CAUSAL, SPLIT, SCHED != 2, SCHED == 3>(p, bh, qb, split, smem);
   } else {
     attention_tile_loop<Pol, WAVES, CAUSAL, SPLIT>(p, bh, qb, split, smem);
   }
@@ -244,7 +245,8 @@ constexpr kernel_fn pick_kernel() {
 // DT: 0 = fp16, 1 = bf16 (FA_DTYPE_*)
 // LDS images keep 256-B row slots at head_dim 64 too (fa_fwd_kernel.hpp M16)
 #define FA_CFG_TD(ID, W, BN_, C, KIND, M, SCHED, DT, HDIM, NAME)                           \
-  {{ID, 32 * (W), BN_, W, C, (KIND) == 1, 4 * (BN_) * ROW_BYTES, NAME, DT, HDIM}, M, SCHED, \
+  {{ID, 32 * (W), BN_, W, C, (KIND) == 1, ((SCHED) == 3 ? 6 : 4) * (BN_) * ROW_BYTES, NAME, DT,  \
+    HDIM}, M, SCHED,                                                                        \
    KIND, pick_kernel<W, BN_, C, KIND, M, SCHED, DT, HDIM>()}
 #define FA_CFG_T(ID, W, BN_, C, KIND, M, SCHED, DT, NAME) \
   FA_CFG_TD(ID, W, BN_, C, KIND, M, SCHED, DT, 128, NAME)
@@ -282,6 +284,9 @@ static const Config kConfigs[] = {
     FA_CFG_TD(26, 8, 64, 0, 2, 16, 1, 1, 64,
               "bf16_d64_bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
     FA_CFG_TD(27, 8, 64, 1, 2, 16, 1, 1, 64, "bf16_d64_bm256_bn64_w8_m16_pingpong_persistent_causal"),
+    // K/V by LDS-DMA into three rotating LDS buffers
+    FA_CFG(28, 8, 64, 0, 2, 16, 3, "bm256_bn64_w8_m16_pingpong_persistent_dma_noncausal"),
+    FA_CFG(29, 8, 64, 1, 2, 16, 3, "bm256_bn64_w8_m16_pingpong_persistent_dma_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 

@@ -88,6 +88,29 @@ __device__ __forceinline__ void buf_store16f(__amdgpu_buffer_rsrc_t r, int voff,
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, 0, 0);
 }
 
+// LDS-DMA: one 16-B global load per lane written straight into LDS at
+// lds_base + 16*lane (buffer_load_dwordx4 ... lds; no VGPR destination).
+// Completion is counted by vmcnt like any load.
+// Inline asm, not the builtin: for the builtin hipcc inserts vmcnt(0) before
+// every later LDS read (it cannot tell which buffer the DMA writes), which
+// serialises each MFMA block behind the next tile's load.  The asm is
+// invisible to hipcc's waitcnt bookkeeping, so completion is waited for
+// explicitly (s_waitcnt vmcnt) before the barrier that publishes the tile.
+// M0 (LDS base) is saved and restored inside the statement (hipcc reserves it).
+__device__ __forceinline__ void buf_load16_lds(__amdgpu_buffer_rsrc_t r, void* lds_base, int voff) {
+  const unsigned lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds_base;
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(r)
+      : "memory");
+}
+
 // LDS image A: 8-row x 32-column subtiles of 512 B, 16-B chunk XOR (row>>2)&3.
 // Conflict-free for ds_read_b64_tr_b16 column reads (both MFMA shapes) and
 // for the 32x32x16 ds_read_b128 row reads.
@@ -98,6 +121,16 @@ __device__ __forceinline__ int lds_off(int row, int ch) {
 // LDS image B: plain 256-B rows, chunk XOR (row&15).  Conflict-free for the
 // 16x16x32 ds_read_b128 row reads.
 __device__ __forceinline__ int k_off16(int row, int ch) { return 256 * row + 16 * (ch ^ (row & 15)); }
+// inverses (LDS byte offset o within a tile image -> tile-relative source
+// byte offset row*256 + ch*16), for LDS-DMA, whose destination is lane-linear
+__device__ __forceinline__ int k_off16_src(int o) {
+  const int row = o >> 8;
+  return 256 * row + 16 * (((o >> 4) & 15) ^ (row & 15));
+}
+__device__ __forceinline__ int lds_off_src(int o) {
+  const int row = 8 * (o >> 11) + ((o >> 6) & 7);
+  return 256 * row + 16 * (4 * ((o >> 9) & 3) + (((o >> 4) & 3) ^ ((row >> 2) & 3)));
+}
 
 __device__ __forceinline__ float max_xor32(float x) {
   // lanes l and l^32 exchange; r[0] = {x[0..31], x[0..31]}, r[1] = {x[32..63], x[32..63]}
@@ -479,6 +512,8 @@ struct M16 {
   }
   static __device__ __forceinline__ int k_lds(int row, int ch) { return k_off16(row, ch); }
   static __device__ __forceinline__ int v_lds(int row, int ch) { return lds_off(row, ch); }
+  static __device__ __forceinline__ int k_src(int o) { return k_off16_src(o); }
+  static __device__ __forceinline__ int v_src(int o) { return lds_off_src(o); }
 
   __device__ __forceinline__ void qk(const char* kb) {
 #pragma unroll
@@ -816,7 +851,10 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
 // first read in half-step 2k+2 and their buffers were last read in half-step
 // 2k-1, so two buffers suffice.
 // ---------------------------------------------------------------------------
-template <class Pol, bool CAUSAL, bool SPLIT, bool PRIO = true>
+// DMA: K/V tiles go global -> LDS by LDS-DMA into three rotating buffers
+// (a tile's buffer must be free when its loads are issued, one half-step
+// before the register path would write it), no staging registers.
+template <class Pol, bool CAUSAL, bool SPLIT, bool PRIO = true, bool DMA = false>
 __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, int qb, int split,
                                                    char* smem) {
   constexpr int WAVES = 8;
@@ -855,7 +893,8 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   // phase (causal), or at the end of the softmax phase, by the wave whose
   // phase is the shorter one (non-causal: +2 % at S=8192; causal: -5 %, its
   // masked/inactive tiles shorten the MFMA phases instead)
-  constexpr bool kIssueInSm = !CAUSAL;
+  constexpr bool kIssueInSm = DMA || !CAUSAL;  // DMA: legal with three buffers
+  static_assert(!DMA || Pol::HDIM == 128, "LDS-DMA path: head_dim 128");
 
 #ifdef FA_STAMPS
   const unsigned long long t_in = __builtin_amdgcn_s_memtime();
@@ -864,8 +903,20 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   pol.init(lane, p.c);
   pol.issue_q(make_rsrc(Qh, S * ROW_BYTES), qw);  // scaled once K_0 / tile 0 are in flight
 
+  constexpr int NBUF = DMA ? 3 : 2;  // tile buffers per tensor
   char* kbuf0 = smem;
-  char* vbuf0 = smem + 2 * TILE_BYTES;
+  char* vbuf0 = smem + NBUF * TILE_BYTES;
+  auto kbuf = [&](int x) { return kbuf0 + (DMA ? x % 3 : x & 1) * TILE_BYTES; };
+  auto vbuf = [&](int x) { return vbuf0 + (DMA ? (x + 3) % 3 : x & 1) * TILE_BYTES; };
+  // LDS-DMA: this wave's 1-KB pieces of a tile image (pieces wave, wave + 8, ...)
+  int k_src[NCH], v_src[NCH];
+  if constexpr (DMA) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      k_src[i] = Pol::k_src(1024 * (wave + WAVES * i) + 16 * lane);
+      v_src[i] = Pol::v_src(1024 * (wave + WAVES * i) + 16 * lane);
+    }
+  }
   const int kr0 = pol.k_stage_row(wave), kc = pol.k_stage_ch();
   const int vr0 = pol.v_stage_row(wave), vc = pol.v_stage_ch();
   f16x8 kst[NCH], vst[NCH];
@@ -874,19 +925,33 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     const int kb_row = kv_lo + (k + 1) * BN, vb_row = kv_lo + k * BN;
     const auto rk = make_rsrc(Kh + (size_t)kb_row * HD, (kv_hi - kb_row) * ROW_BYTES);
     const auto rv = make_rsrc(Vh + (size_t)vb_row * HD, (kv_hi - vb_row) * ROW_BYTES);
+    if constexpr (DMA) {
+      char* kb = kbuf(k + 1);
+      char* vb = vbuf(k);
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      kst[i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
-      vst[i] = buf_load16(rv, (vr0 + Pol::RPW * WAVES * i) * ROW_BYTES + vc * 16);
+      for (int i = 0; i < NCH; ++i) {
+        buf_load16_lds(rk, kb + 1024 * (wave + WAVES * i), k_src[i]);
+        buf_load16_lds(rv, vb + 1024 * (wave + WAVES * i), v_src[i]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        kst[i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
+        vst[i] = buf_load16(rv, (vr0 + Pol::RPW * WAVES * i) * ROW_BYTES + vc * 16);
+      }
     }
   };
   auto write_tile = [&](int k) {
-    char* kb = kbuf0 + ((k + 1) & 1) * TILE_BYTES;
-    char* vb = vbuf0 + (k & 1) * TILE_BYTES;
+    if constexpr (DMA) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's pieces of tile k have landed
+    } else {
+      char* kb = kbuf(k + 1);
+      char* vb = vbuf(k);
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      *reinterpret_cast<f16x8*>(kb + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = kst[i];
-      *reinterpret_cast<f16x8*>(vb + Pol::v_lds(vr0 + Pol::RPW * WAVES * i, vc)) = vst[i];
+      for (int i = 0; i < NCH; ++i) {
+        *reinterpret_cast<f16x8*>(kb + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = kst[i];
+        *reinterpret_cast<f16x8*>(vb + Pol::v_lds(vr0 + Pol::RPW * WAVES * i, vc)) = vst[i];
+      }
     }
   };
 
@@ -918,8 +983,7 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     // the MFMA-phase wave wins VALU/MFMA issue arbitration against its SIMD
     // partner (which is in its softmax phase), so its matrix stream stays dense
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-    pol.mfma_block(kbuf0 + (k & 1) * TILE_BYTES, vbuf0 + ((k - 1) & 1) * TILE_BYTES,
-                   k >= 1 && active(k - 1), k < n && active(k));
+    pol.mfma_block(kbuf(k), vbuf(k - 1), k >= 1 && active(k - 1), k < n && active(k));
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   };
   auto softmax_block = [&](int k) {

@@ -1,4 +1,5 @@
-"""Persistent kernel (one workgroup per CU walking its XCD's query blocks):
+"""Persistent kernels (one workgroup per CU walking its XCD's query blocks;
+register-staged K/V, and the LDS-DMA variant with three rotating buffers):
 shapes where every workgroup walks SEVERAL query blocks, including ragged
 sequence lengths, head counts that are not a multiple of the 8 XCD groups,
 and single-tile items.
@@ -41,8 +42,11 @@ def _ids(kind_name):
     fa = _fa()
     out = {}
     for c in fa.configs():
-        if kind_name in c.name and c.dtype == "float16" and c.head_dim == 128:
+        if c.dtype == "float16" and c.head_dim == 128 and c.name in (
+                f"bm256_bn64_w8_m16_pingpong_{kind_name}_noncausal",
+                f"bm256_bn64_w8_m16_pingpong_{kind_name}_causal"):
             out[c.causal] = c.id
+    assert set(out) == {False, True}, kind_name
     return out
 
 
@@ -57,7 +61,7 @@ SHAPES = [
 
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
-@pytest.mark.parametrize("kind", ["persistent"])
+@pytest.mark.parametrize("kind", ["persistent", "persistent_dma"])
 def test_persistent_bit_identical(kind, shape, causal):
     fa = _fa()
     b, h, s = shape
