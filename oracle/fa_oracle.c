@@ -83,13 +83,15 @@ void fa_oracle_gen_inputs(uint16_t* q, uint16_t* k, uint16_t* v, size_t n,
 
 /* ---- cpu_attention: flash_attention.cu:668-697, one (b,h) head ---- */
 
-static void attention_one_head(const uint16_t* q, const uint16_t* k,
-                               const uint16_t* v, uint16_t* o, int seq_len,
-                               int head_dim, int causal, float* scores,
-                               float* qrow) {
+/* rows [row_begin, row_end) of one head; rows are independent, so a head can
+   be split over threads without changing any row's operation order */
+static void attention_rows(const uint16_t* q, const uint16_t* k,
+                           const uint16_t* v, uint16_t* o, int seq_len,
+                           int head_dim, int causal, int row_begin, int row_end,
+                           float* scores, float* qrow) {
   /* :670 scale = 1/sqrtf(head_dim) */
   const float scale = 1.0f / sqrtf((float)head_dim);
-  for (int i = 0; i < seq_len; i++) {
+  for (int i = row_begin; i < row_end; i++) {
     /* __half2float(q[i*hd+d]) hoisted: same values, same order of use */
     for (int d = 0; d < head_dim; d++)
       qrow[d] = fa_oracle_f16_to_f32(q[(size_t)i * head_dim + d]);
@@ -125,13 +127,24 @@ void fa_oracle_attention_heads(const uint16_t* q, const uint16_t* k,
                                int causal, int n_threads) {
   if (n_threads < 1) n_threads = 1;
   const size_t stride = (size_t)seq_len * head_dim;
-#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads)
-  for (int bh = bh_begin; bh < bh_end; bh++) {
+  /* work item = (head, 64-row chunk): one head alone still uses every thread */
+  const int chunk = 64;
+  const int nchunk = (seq_len + chunk - 1) / chunk;
+  const long long items = (long long)(bh_end - bh_begin) * nchunk;
+#pragma omp parallel num_threads(n_threads)
+  {
     float* scores = (float*)malloc((size_t)seq_len * sizeof(float));
     float* qrow = (float*)malloc((size_t)head_dim * sizeof(float));
-    attention_one_head(q + bh * stride, k + bh * stride, v + bh * stride,
-                       o + bh * stride, seq_len, head_dim, causal, scores,
-                       qrow);
+#pragma omp for schedule(dynamic, 1)
+    for (long long it = 0; it < items; it++) {
+      /* causal: heaviest (last) chunks first for balance */
+      const int bh = bh_begin + (int)(it / nchunk);
+      const int c = nchunk - 1 - (int)(it % nchunk);
+      const int r1 = (c + 1) * chunk < seq_len ? (c + 1) * chunk : seq_len;
+      attention_rows(q + bh * stride, k + bh * stride, v + bh * stride,
+                     o + bh * stride, seq_len, head_dim, causal, c * chunk, r1,
+                     scores, qrow);
+    }
     free(qrow);
     free(scores);
   }

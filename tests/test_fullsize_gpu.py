@@ -65,7 +65,7 @@ def test_config5_full_size_sampled_heads():
 
 @pytest.mark.parametrize("s,causal", [(16384, True), (8192, False)])
 def test_long_sequences_sampled_heads(s, causal):
-    _check_sampled(1, 32, s, causal, [0, 13, 31], seed=11)
+    _check_sampled(1, 32, s, causal, [0, 31], seed=11)
 
 
 @pytest.mark.parametrize("causal", [False, True])
