@@ -177,6 +177,18 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(Fw
   }
 }
 
+// KV-pair (short sequences): 128 query rows per workgroup, the two waves of a
+// SIMD split the key range (attention_kvpair); one workgroup per item, items
+// ordered as map_block.
+template <int BN, bool CAUSAL, bool BF16 = false, int HDIM = 128>
+__global__ __launch_bounds__(512, 2) void fa_fwd_f16_kvpair_kernel(FwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using Pol = M16<BN, typename std::conditional<BF16, __bf16, f16>::type, HDIM>;
+  int qb, bh;
+  map_block(blockIdx.x, gridDim.x, p.nqb, p.bh, p.band, CAUSAL, qb, bh);
+  attention_kvpair<Pol, CAUSAL>(p, bh, qb, smem);
+}
+
 // Split-KV: workgroup id -> (split, item); items ordered as map_block.
 template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED>
 __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_splitkv_kernel(FwdParams p) {
@@ -227,13 +239,15 @@ struct Config {
   fa_config_info_t info;
   int mfma;   // 32 = v_mfma_f32_32x32x16_f16 loop, 16 = v_mfma_f32_16x16x32_f16 loop
   int sched;  // 0 = one barrier per tile, 1 = 8-wave ping-pong
-  int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent
+  int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent, 3 = KV-pair
   kernel_fn fn;
 };
 
 template <int W, int BN_, int C, int SPL, int M, int SCHED, int DT, int HDIM>
 constexpr kernel_fn pick_kernel() {
-  if constexpr (SPL == 1)
+  if constexpr (SPL == 3)
+    return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
+  else if constexpr (SPL == 1)
     return fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
   else if constexpr (SPL == 2)
     return fa_fwd_f16_persistent_kernel<W, BN_, (C != 0), (M == 16), SCHED, DT == 1, HDIM>;
@@ -251,6 +265,10 @@ constexpr kernel_fn pick_kernel() {
 #define FA_CFG_T(ID, W, BN_, C, KIND, M, SCHED, DT, NAME) \
   FA_CFG_TD(ID, W, BN_, C, KIND, M, SCHED, DT, 128, NAME)
 #define FA_CFG(ID, W, BN_, C, KIND, M, SCHED, NAME) FA_CFG_T(ID, W, BN_, C, KIND, M, SCHED, 0, NAME)
+// KV-pair: 8 waves on 128 query rows (two waves per row block, key range split)
+#define FA_CFG_KVPAIR(ID, C, DT, HDIM, NAME)                                           \
+  {{ID, 128, 64, 8, C, 0, kKvpairLdsBytes, NAME, DT, HDIM}, 16, 1, 3,                   \
+   pick_kernel<8, 64, C, 3, 16, 1, DT, HDIM>()}
 
 static const Config kConfigs[] = {
     FA_CFG(0, 4, 64, 0, 0, 32, 0, "bm128_bn64_w4_m32_noncausal"),
@@ -287,6 +305,15 @@ static const Config kConfigs[] = {
     // K/V by LDS-DMA into three rotating LDS buffers
     FA_CFG(28, 8, 64, 0, 2, 16, 3, "bm256_bn64_w8_m16_pingpong_persistent_dma_noncausal"),
     FA_CFG(29, 8, 64, 1, 2, 16, 3, "bm256_bn64_w8_m16_pingpong_persistent_dma_causal"),
+    // KV-pair (short sequences): the two waves of a SIMD split the keys of 32 query rows
+    FA_CFG_KVPAIR(30, 0, 0, 128, "bm128_bn64_w8_m16_kvpair_noncausal"),
+    FA_CFG_KVPAIR(31, 1, 0, 128, "bm128_bn64_w8_m16_kvpair_causal"),
+    FA_CFG_KVPAIR(32, 0, 1, 128, "bf16_bm128_bn64_w8_m16_kvpair_noncausal"),
+    FA_CFG_KVPAIR(33, 1, 1, 128, "bf16_bm128_bn64_w8_m16_kvpair_causal"),
+    FA_CFG_KVPAIR(34, 0, 0, 64, "d64_bm128_bn64_w8_m16_kvpair_noncausal"),
+    FA_CFG_KVPAIR(35, 1, 0, 64, "d64_bm128_bn64_w8_m16_kvpair_causal"),
+    FA_CFG_KVPAIR(36, 0, 1, 64, "bf16_d64_bm128_bn64_w8_m16_kvpair_noncausal"),
+    FA_CFG_KVPAIR(37, 1, 1, 64, "bf16_d64_bm128_bn64_w8_m16_kvpair_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -430,12 +457,15 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   //  * 8-wave persistent ping-pong (256 rows / workgroup) once there are two
   //    256-row items per CU, or one per CU without a mask (S=2048 B=1 H=32
   //    non-causal: 1015 vs 873 TFLOP/s);
-  //  * otherwise 4-wave 16x16x32 (128 rows), which keeps more CUs busy on the
-  //    short, latency-bound launches (S <= 2048 causal at B=1 H=32).
+  //  * otherwise the KV-pair kernel (128 rows per workgroup, the two waves of
+  //    a SIMD splitting the keys): twice the workgroups of the 256-row tier
+  //    and half the heaviest causal key loop on the short, under-filled
+  //    launches; 1.0-1.2x the 4-wave 128-row loop it replaces at B=1 H=32,
+  //    S=512-2048 (profiles/r01_short_s_ab.jsonl).
   const long long bh = (long long)batch * heads;
   const long long wg256 = bh * ((seq_len + 255) / 256);
   if (wg256 >= 512 || (!causal && wg256 >= 256)) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 2);
-  return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
+  return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 3);
 }
 
 namespace fa {
@@ -565,7 +595,7 @@ extern "C" const char* fa_status_string(int status) {
   switch (status) {
     case FA_OK: return "ok";
     case FA_ERR_NULL_POINTER: return "null device pointer";
-    case FA_ERR_UNSUPPORTED_HEAD_DIM: return "unsupported head_dim (only 128)";
+    case FA_ERR_UNSUPPORTED_HEAD_DIM: return "unsupported head_dim (128 or 64)";
     case FA_ERR_BAD_SHAPE: return "bad shape";
     case FA_ERR_LAUNCH: return "kernel launch failed";
     case FA_ERR_BAD_CONFIG: return "bad tile config";
@@ -588,7 +618,8 @@ extern "C" int fa_debug_stamps(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fa::g_fa_stamps), sizeof(fa::g_fa_stamps)) != hipSuccess)
     return FA_ERR_HIP;
   if (reset) {
-    static const unsigned long long z[8][5] = {};
+    static const unsigned long long z[8][12] = {};
+    static_assert(sizeof(z) == sizeof(fa::g_fa_stamps), "reset covers every stamp");
     if (hipMemcpyToSymbol(HIP_SYMBOL(fa::g_fa_stamps), z, sizeof(z)) != hipSuccess) return FA_ERR_HIP;
   }
   return FA_OK;

@@ -54,6 +54,8 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 constexpr int HD = 128;            // head_dim (the reference hard-codes 128, :613)
 constexpr int ROW_BYTES = HD * 2;  // one K/V/Q row in bytes
 constexpr float RESCALE_LOG2 = 8.0f;
+// attention_kvpair: 4 tile buffers (64 KB) or the merge region (4 x 17 KB at head_dim 128)
+constexpr int kKvpairLdsBytes = 4 * (2 * 8 + 1) * 64 * 16;
 
 struct FwdParams {
   const f16* q;
@@ -232,6 +234,8 @@ struct M32 {
     for (int t = 0; t < 8; ++t)
 #pragma unroll
       for (int j = 0; j < 8; ++j) qf[t][j] = (f16)((float)qf[t][j] * c);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) asm volatile("" : "+v"(qf[t]));  // see M16::pin_q
   }
   __device__ __forceinline__ void load_q(__amdgpu_buffer_rsrc_t rq, int qw) {
     issue_q(rq, qw);
@@ -490,6 +494,16 @@ struct M16 {
       for (int t = 0; t < NTQ; ++t)
 #pragma unroll
         for (int j = 0; j < 8; ++j) qf[b][t][j] = (T)((float)qf[b][t][j] * c);
+    pin_q();
+  }
+  // materialise the scaled Q here: otherwise hipcc sinks the scaling VALU past
+  // the prologue barrier to the first MFMA, where its vmcnt waits also cover
+  // every tile load issued since (a full memory latency per item)
+  __device__ __forceinline__ void pin_q() {
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int t = 0; t < NTQ; ++t) asm volatile("" : "+v"(qf[b][t]));
   }
   __device__ __forceinline__ void load_q(__amdgpu_buffer_rsrc_t rq, int qw) {
     issue_q(rq, qw);
@@ -693,12 +707,20 @@ struct M16 {
     return lacc[b][0];  // already the full row sum (MFMA over all keys)
 #endif
   }
+  // Epilogue: lane (g, r16) holds d = 16e + 4g + 0..3 of row r16 for every e.
+  // One v_permlane16_swap per dword of a d-block pair (e, e+1) exchanges the
+  // odd 16-lane rows of block e with the even rows of block e+1, leaving each
+  // lane 8 contiguous d of one row: g0 -> 16e+0..7, g1 -> 16(e+1)+0..7,
+  // g2 -> 16e+8..15, g3 -> 16(e+1)+8..15.  Half the store instructions
+  // (dwordx4 instead of dwordx2) at the same bytes; the store tail is
+  // issue-bound (guide T21).
   __device__ __forceinline__ void store_o(__amdgpu_buffer_rsrc_t ro, int qw) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const float lt = row_sum(b);  // already the full row sum (MFMA over all keys)
       const float inv = lt > 0.f ? 1.0f / lt : 0.f;
       const int rowb = (qw + 16 * b + r16) * ROW;
+#ifdef FA_NARROW_STORE
 #pragma unroll
       for (int e = 0; e < NE; ++e) {
         tx4 w;
@@ -706,6 +728,61 @@ struct M16 {
         for (int x = 0; x < 4; ++x) w[x] = (T)(acc[b][e][x] * inv);
         buf_store8(ro, rowb + 2 * (16 * e + 4 * g), __builtin_bit_cast(f16x4, w));
       }
+#else
+      const int dlane = 16 * (g & 1) + 8 * (g >> 1);
+#pragma unroll
+      for (int ep = 0; ep < NE / 2; ++ep) {
+        tx4 wx, wy;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          wx[x] = (T)(acc[b][2 * ep][x] * inv);
+          wy[x] = (T)(acc[b][2 * ep + 1][x] * inv);
+        }
+        u32x2 X = __builtin_bit_cast(u32x2, wx), Y = __builtin_bit_cast(u32x2, wy);
+#pragma unroll
+        for (int dw = 0; dw < 2; ++dw) {
+          const auto r = __builtin_amdgcn_permlane16_swap(X[dw], Y[dw], false, false);
+          X[dw] = r[0];
+          Y[dw] = r[1];
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{X[0], X[1], Y[0], Y[1]}, ro,
+                                               rowb + 2 * (32 * ep + dlane), 0, 0);
+      }
+#endif
+    }
+  }
+  // KV-pair merge (attention_kvpair): the partner wave's state goes through LDS
+  // lane-linearly (both waves hold the same query rows in the same lanes).
+  // Region per wave: 2*NE f32x4 of O, then one f32x4 {m_0, l_0, m_1, l_1}.
+  static constexpr int MERGE_BYTES = (2 * NE + 1) * 64 * 16;
+#ifdef FA_ROWSUM_VALU
+#error "KV-pair merge assumes MFMA row sums (lacc holds the full row sum)"
+#endif
+  __device__ __forceinline__ void put_partial(char* region) const {
+    f32x4* d = reinterpret_cast<f32x4*>(region);
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < NE; ++e) d[(b * NE + e) * 64 + lane] = acc[b][e];
+    d[2 * NE * 64 + lane] = f32x4{m_ref[0], lacc[0][0], m_ref[1], lacc[1][0]};
+  }
+  // O = O_a 2^(m_a-M) + O_b 2^(m_b-M), l likewise, M = max over partials that saw a key
+  __device__ __forceinline__ void merge_partial(const char* region) {
+    const f32x4* d = reinterpret_cast<const f32x4*>(region);
+    const f32x4 ml = d[2 * NE * 64 + lane];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const float la = lacc[b][0], lb = ml[2 * b + 1];
+      const float ma = la > 0.f ? m_ref[b] : ninf();
+      const float mb = lb > 0.f ? ml[2 * b] : ninf();
+      float M = fmaxf(ma, mb);
+      M = M == ninf() ? 0.f : M;
+      const float wa = __builtin_amdgcn_exp2f(ma - M), wb = __builtin_amdgcn_exp2f(mb - M);
+#pragma unroll
+      for (int e = 0; e < NE; ++e) acc[b][e] = acc[b][e] * wa + d[(b * NE + e) * 64 + lane] * wb;
+      const float l = la * wa + lb * wb;
+      lacc[b] = f32x4{l, l, l, l};
+      m_ref[b] = M;
     }
   }
   // m in the reference's units (scaled score, natural log): m_ref * ln 2
@@ -767,7 +844,7 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
 
   Pol pol;
   pol.init(lane, p.c);
-  pol.load_q(make_rsrc(Qh, S * ROW_BYTES), qw);
+  pol.issue_q(make_rsrc(Qh, S * ROW_BYTES), qw);  // scaled once tile 0's loads are in flight
 
   // staging offsets (compile-time slot i adds 4*WAVES rows)
   const int kr0 = pol.k_stage_row(wave), kc = pol.k_stage_ch();
@@ -796,6 +873,11 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
   // prologue: unconditional, so every earlier load (Q included) has retired
   // before the loop and no in-loop MFMA waits on the prefetch
   issue_loads(kv_lo);
+  // every prologue load is issued before the first VALU that waits on one
+  // (else the scheduler hoists Q's scaling above the K/V loads: two serial
+  // memory latencies per item)
+  __builtin_amdgcn_sched_barrier(0);
+  pol.scale_q();
   write_lds(smem);
   // vmcnt(0): the compiler may order the Q loads after the K/V loads; without
   // this, its waitcnt analysis keeps Q "pending" at the loop header and every
@@ -894,6 +976,11 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   // phase is the shorter one (non-causal: +2 % at S=8192; causal: -5 %, its
   // masked/inactive tiles shorten the MFMA phases instead)
   constexpr bool kIssueInSm = DMA || !CAUSAL;  // DMA: legal with three buffers
+  // where a tile is written to LDS: at the start of the softmax phase (beside
+  // the partner's MFMAs; causal: +0.3-0.7 % A/B) or at its end (non-causal:
+  // early was -0.8 %, its loads are issued in the softmax phase and need it
+  // to land)
+  constexpr bool kWriteEarly = CAUSAL && !DMA;
   static_assert(!DMA || Pol::HDIM == 128, "LDS-DMA path: head_dim 128");
 
 #ifdef FA_STAMPS
@@ -964,6 +1051,7 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     for (int i = 0; i < NCH; ++i)
       k0[i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
     if ((kIssueInSm || grp == 1) && n > 0) issue_tile(0);
+    __builtin_amdgcn_sched_barrier(0);  // all prologue loads issued first (attention_tile_loop)
     pol.scale_q();
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
@@ -1028,6 +1116,10 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     FA_STAMP(st1);
     __syncthreads();
     FA_STAMP(st2);
+    if constexpr (kWriteEarly) {
+      if (t < n) write_tile(t);
+      if (kIssueInSm && t + 1 < n) issue_tile(t + 1);
+    }
     softmax_block(k);
 #ifdef FA_STAMPS
     unsigned long long st25;
@@ -1039,8 +1131,10 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     FA_STAMP(st_w);
     st_acc[10] += st_w - st25;
 #endif
-    if (t < n) write_tile(t);
-    if (kIssueInSm && t + 1 < n) issue_tile(t + 1);
+    if constexpr (!kWriteEarly) {
+      if (t < n) write_tile(t);
+      if (kIssueInSm && t + 1 < n) issue_tile(t + 1);
+    }
     FA_STAMP(st3);
     __syncthreads();
     FA_STAMP(st4);
@@ -1075,6 +1169,210 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
 #undef FA_STAMP
 }
 
+// ---------------------------------------------------------------------------
+// KV-pair skeleton (8 waves, 128 query rows): short sequences.
+// The two waves of a SIMD hold the SAME 32 query rows and split the key range
+// between them -- wave w (group A) takes key tiles 0, 2, 4, ..., wave w+4
+// (group B) tiles 1, 3, 5, ... -- and merge (O, m, l) through LDS at the end.
+// Half the query rows per workgroup of the 256-row ping-pong, so twice the
+// workgroups on a short launch (S=1024, B=1, H=32: 256 instead of 128, one
+// per CU), and the heaviest causal block's key loop is halved.
+//
+// Every wave runs the ping-pong phase pair [MFMA] barrier [softmax] barrier,
+// group B one half-step behind group A.  On the shared half-step clock h:
+//   MFMA phase at h (group h & 1): QK^T of tile h, PV of tile h-2
+//   softmax phase at h:            tile h-1 (the other group's QK^T of h-1)
+// so K_t is read only at half-step t and V_t only at t+2: at the end of
+// half-step h every wave writes its staged share of stage h = (K_{h+1},
+// V_{h-1}) (one tile of each per half-step, two LDS buffers per tensor) and
+// issues the loads of stage h+2, two half-steps ahead (two staging sets: one
+// for the wave's MFMA half-steps, one for its softmax half-steps).
+// Measured and not kept: only the softmax-phase group staging each tile, at
+// the start of its phase (-1.5 %, the softmax side is already the long pole);
+// one staging set, loads one half-step ahead (equal).
+// ---------------------------------------------------------------------------
+template <class Pol, bool CAUSAL>
+__device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int qb, char* smem) {
+  constexpr int WAVES = 8;
+  constexpr int BN = Pol::BN;
+  constexpr int NT = WAVES * 64;
+  constexpr int BM = 128;
+  constexpr int HD = Pol::HDIM;
+  constexpr int ROW_BYTES = 2 * HD;
+  constexpr int TILE_BYTES = BN * 256;
+  constexpr int NCH = (BN * (HD / 8)) / NT;
+  static_assert((BN * (HD / 8)) % NT == 0, "tile chunks must divide evenly");
+  static_assert(4 * Pol::MERGE_BYTES <= kKvpairLdsBytes, "merge region fits the LDS allocation");
 
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2;  // 0 = A (even tiles), 1 = B (odd tiles)
+  const int rw = wave & 3;    // row wave: both groups hold rows q0 + 32 rw ...
+  const int S = p.seq_len;
+
+  const size_t head_off = (size_t)bh * (size_t)S * HD;
+  const f16* Qh = p.q + head_off;
+  const f16* Kh = p.k + head_off;
+  const f16* Vh = p.v + head_off;
+
+  const int q0 = qb * BM;
+  const int qw = q0 + rw * 32;
+  const int kv_hi = CAUSAL ? min(q0 + BM, S) : S;
+  const int n = (kv_hi + BN - 1) / BN;
+
+#ifdef FA_STAMPS
+  unsigned long long st_acc[11] = {}, sa, sb;
+  const unsigned long long t_in = __builtin_amdgcn_s_memtime();
+#define FA_KSTAMP(v)                                                          \
+  do {                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+  } while (0)
+#else
+#define FA_KSTAMP(v) \
+  do {               \
+  } while (0)
+#endif
+
+  Pol pol;
+  pol.init(lane, p.c);
+  pol.issue_q(make_rsrc(Qh, S * ROW_BYTES), qw);
+
+  auto kbuf = [&](int x) { return smem + (x & 1) * TILE_BYTES; };
+  auto vbuf = [&](int x) { return smem + (2 + (x & 1)) * TILE_BYTES; };
+  const int kr0 = pol.k_stage_row(wave), kc = pol.k_stage_ch();
+  const int vr0 = pol.v_stage_row(wave), vc = pol.v_stage_ch();
+  // staging set 0 carries the stages of this wave's MFMA half-steps, set 1
+  // those of its softmax half-steps (they alternate)
+  f16x8 kst[2][NCH], vst[2][NCH];
+  // loads of stage h = (K_{h+1}, V_{h-1}); rows at/after kv_hi, and tiles
+  // outside [0, n), read as 0 with no memory traffic
+  auto issue_stage = [&](int h, auto set_c) {
+    constexpr int X = decltype(set_c)::value;
+    const int kb_row = (h + 1) * BN, vb_row = (h - 1) * BN;
+    const auto rk = make_rsrc(Kh + (size_t)min(kb_row, S) * HD, (kv_hi - kb_row) * ROW_BYTES);
+    const auto rv = make_rsrc(Vh + (size_t)max(vb_row, 0) * HD,
+                              vb_row < 0 ? 0 : (kv_hi - vb_row) * ROW_BYTES);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      kst[X][i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
+      vst[X][i] = buf_load16(rv, (vr0 + Pol::RPW * WAVES * i) * ROW_BYTES + vc * 16);
+    }
+  };
+  auto write_stage = [&](int h, auto set_c) {
+    constexpr int X = decltype(set_c)::value;
+    char* kb = kbuf(h + 1);
+    char* vb = vbuf(h - 1);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      *reinterpret_cast<f16x8*>(kb + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = kst[X][i];
+      *reinterpret_cast<f16x8*>(vb + Pol::v_lds(vr0 + Pol::RPW * WAVES * i, vc)) = vst[X][i];
+    }
+  };
+  using Set0 = std::integral_constant<int, 0>;
+  using Set1 = std::integral_constant<int, 1>;
+
+  // prologue: Q, K_0 and the first two stages' loads in flight together
+  {
+    const auto rk = make_rsrc(Kh, kv_hi * ROW_BYTES);
+    f16x8 k0[NCH];
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      k0[i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
+    // set 0 = this wave's first MFMA half-step (A: h=0, B: h=1), set 1 = its
+    // first softmax one (A: h=1, B: the idle h=0); branch-free: a per-group
+    // branch makes hipcc merge the paths with register copies that wait for
+    // the loads
+    issue_stage(grp, Set0{});
+    issue_stage(1 - grp, Set1{});
+    __builtin_amdgcn_sched_barrier(0);  // all prologue loads issued first (attention_tile_loop)
+    pol.scale_q();
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      *reinterpret_cast<f16x8*>(kbuf(0) + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = k0[i];
+  }
+  // Q and K_0 retired (see attention_tile_loop); the stage loads may stay in flight
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (4 * NCH));
+  __syncthreads();
+#ifdef FA_STAMPS
+  st_acc[7] = __builtin_amdgcn_s_memtime() - t_in;
+#endif
+
+  const float c = p.c;
+  auto active = [&](int t) { return t >= 0 && t < n && (!CAUSAL || t * BN <= qw + 31); };
+  // end of half-step h: publish its stage, refill the staging set, barrier
+  auto half_step_end = [&](int h, auto set_c, int bar_slot) {
+#ifdef FA_STAMPS
+    unsigned long long w0, w1, w2, w3;
+    FA_KSTAMP(w0);
+    __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * NCH));
+    FA_KSTAMP(w1);
+#endif
+    write_stage(h, set_c);
+    issue_stage(h + 2, set_c);
+#ifdef FA_STAMPS
+    FA_KSTAMP(w2);
+#endif
+    __syncthreads();
+#ifdef FA_STAMPS
+    FA_KSTAMP(w3);
+    st_acc[10] += w1 - w0;
+    st_acc[4] += w2 - w1;
+    st_acc[bar_slot] += w3 - w2;
+#endif
+    (void)bar_slot;
+  };
+  // pairs of half-steps per wave: covers h = 0 .. n+1 (the last PV is at n+1)
+  const int P = (n + 3) >> 1;
+  if (grp == 1) half_step_end(0, Set1{}, 3);  // group B: idle leading half-step
+  for (int m = 0; m < P; ++m) {
+    const int h = 2 * m + grp;
+    FA_KSTAMP(sa);
+    __builtin_amdgcn_s_setprio(1);
+    pol.mfma_block(kbuf(h), vbuf(h - 2), active(h - 2), active(h));
+    __builtin_amdgcn_s_setprio(0);
+    FA_KSTAMP(sb);
+#ifdef FA_STAMPS
+    st_acc[0] += sb - sa;
+#endif
+    half_step_end(h, Set0{}, 1);
+    FA_KSTAMP(sa);
+    if (active(h)) {
+      const int kv0 = h * BN;
+      const bool need_mask = (kv0 + BN > kv_hi) || (CAUSAL && kv0 + BN - 1 > qw);
+      pol.template softmax<CAUSAL>(kv0, kv_hi, qw, c, need_mask);
+    }
+    FA_KSTAMP(sb);
+#ifdef FA_STAMPS
+    st_acc[2] += sb - sa;
+    st_acc[6] += 1;
+#endif
+    half_step_end(h + 1, Set1{}, 3);
+  }
+  if (grp == 0) half_step_end(2 * P, Set0{}, 1);  // group A: idle trailing half-step
+  __builtin_amdgcn_s_waitcnt(0x0F70);            // the last (zero-size) stage loads
+#ifdef FA_STAMPS
+  const unsigned long long t_le = __builtin_amdgcn_s_memtime();
+#endif
+
+  // merge: group B parks its partial state, group A combines and stores
+  char* region = smem + rw * Pol::MERGE_BYTES;
+  if (grp == 1) pol.put_partial(region);
+  __syncthreads();
+  if (grp == 0) {
+    pol.merge_partial(region);
+    pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);
+  }
+#ifdef FA_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  st_acc[8] = __builtin_amdgcn_s_memtime() - t_le;
+  st_acc[9] = 1;
+  if (lane == 0 && blockIdx.x < 64)
+    for (int i = 0; i < 11; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
+#endif
+#undef FA_KSTAMP
+}
 
 }  // namespace fa

@@ -66,8 +66,14 @@ def test_config_table():
     assert [c.id for c in cfgs] == list(range(len(cfgs)))
     for c in cfgs:
         assert c.head_dim in (64, 128) and c.dtype in ("float16", "bfloat16")
-        assert c.block_m == 32 * c.waves
         assert c.block_n % 32 == 0
+        if "_kvpair_" in c.name:
+            # two waves per 32 query rows; LDS = 4 tile buffers or the merge
+            # region (4 waves x (16 O + 1 m/l) x 64 lanes x 16 B), the larger
+            assert c.block_m == 16 * c.waves
+            assert c.lds_bytes == max(4 * c.block_n * 256, 4 * 17 * 64 * 16)
+            continue
+        assert c.block_m == 32 * c.waves
         # K and V image buffers of 256-B row slots: double-buffered, or three
         # rotating buffers each for the LDS-DMA configs
         nbuf = 3 if "_dma_" in c.name else 2
@@ -87,6 +93,10 @@ def test_select_config(causal):
             cid = fa.select_config(b, h, s, causal)
             c = cfgs[cid]
             assert c.causal == causal and not c.split_kv
+    # B=1 H=32: the short, under-filled launches go to the KV-pair kernel,
+    # the long ones to the 256-row persistent ping-pong
+    assert "_kvpair_" in cfgs[fa.select_config(1, 32, 1024, causal)].name
+    assert "_persistent_" in cfgs[fa.select_config(1, 32, 8192, causal)].name
 
 
 def _null_call(lib, head_dim=128, b=1, h=1, s=64, causal=0, ptr=None):
