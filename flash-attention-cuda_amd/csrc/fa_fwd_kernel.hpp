@@ -936,6 +936,12 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
 // DMA: K/V tiles go global -> LDS by LDS-DMA into three rotating buffers
 // (a tile's buffer must be free when its loads are issued, one half-step
 // before the register path would write it), no staging registers.
+// FA_PRIO_MODE (experiment): 0 = s_setprio 1 around every MFMA phase,
+// 1 = none, 2 = static: the younger half (waves 4-7) at priority 1 for the
+// whole loop (guide T5 static form)
+#ifndef FA_PRIO_MODE
+#define FA_PRIO_MODE 0
+#endif
 template <class Pol, bool CAUSAL, bool SPLIT, bool PRIO = true, bool DMA = false>
 __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, int qb, int split,
                                                    char* smem) {
@@ -1070,9 +1076,9 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   auto mfma_block = [&](int k) {
     // the MFMA-phase wave wins VALU/MFMA issue arbitration against its SIMD
     // partner (which is in its softmax phase), so its matrix stream stays dense
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO && FA_PRIO_MODE == 0) __builtin_amdgcn_s_setprio(1);
     pol.mfma_block(kbuf(k), vbuf(k - 1), k >= 1 && active(k - 1), k < n && active(k));
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO && FA_PRIO_MODE == 0) __builtin_amdgcn_s_setprio(0);
   };
   auto softmax_block = [&](int k) {
     if (k < n && active(k)) {
@@ -1086,6 +1092,9 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   // executes one extra barrier first (while A runs MFMA_0) and A one extra at
   // the end, so B trails A by exactly one half-step with no group-specific
   // code path.  Tile t = k + grp is loaded during MFMA_k and written during SM_k.
+  if constexpr (PRIO && FA_PRIO_MODE == 2) {
+    if (grp == 1) __builtin_amdgcn_s_setprio(1);
+  }
   if (grp == 1) {
     if (n > 0) write_tile(0);
     if (kIssueInSm && 1 < n) issue_tile(1);
@@ -1149,6 +1158,7 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
 #endif
   }
   if (grp == 0) __syncthreads();
+  if constexpr (PRIO && FA_PRIO_MODE == 2) __builtin_amdgcn_s_setprio(0);
 #ifdef FA_STAMPS
   const unsigned long long t_le = __builtin_amdgcn_s_memtime();
 #endif
