@@ -454,18 +454,31 @@ using namespace fa;
 extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   // Tier table re-derived for 256 CUs (ref :620-661 picks by seq >= 2048 on
   // 58 SMs), from tools/small_s.py and tools/sweep.py on the box:
-  //  * 8-wave persistent ping-pong (256 rows / workgroup) once there are two
-  //    256-row items per CU, or one per CU without a mask (S=2048 B=1 H=32
-  //    non-causal: 1015 vs 873 TFLOP/s);
-  //  * otherwise the KV-pair kernel (128 rows per workgroup, the two waves of
-  //    a SIMD splitting the keys): twice the workgroups of the 256-row tier
-  //    and half the heaviest causal key loop on the short, under-filled
-  //    launches; 1.0-1.2x the 4-wave 128-row loop it replaces at B=1 H=32,
-  //    S=512-2048 (profiles/r01_short_s_ab.jsonl).
+  //  * 8-wave persistent ping-pong (256 rows / workgroup) once there are
+  //    1.5 256-row items per CU, or one per CU without a mask (S=2048 B=1
+  //    H=32 non-causal: 1015 vs 873 TFLOP/s) or with short items;
+  //  * S <= 128: the 4-wave 128-row loop (a 256-row item would be half
+  //    padding: B=64 H=32 S=128 364 vs 229 TFLOP/s non-causal);
+  //  * under-filled launches (<= 512 128-row blocks): the KV-pair kernel
+  //    (128 rows per workgroup, the two waves of a SIMD splitting the keys):
+  //    twice the workgroups of the 256-row tier and half the heaviest causal
+  //    key loop; 1.0-1.2x the 4-wave loop at B=1 H=32, S=512-2048
+  //    (profiles/r01_short_s_ab.jsonl);
+  //  * otherwise the 4-wave loop (with many blocks the KV-pair's doubled LDS
+  //    traffic per FLOP costs more than its balance gains: B=16 S=512
+  //    causal 4-wave 398 vs KV-pair 294, profiles/r01_tier_study.jsonl).
   const long long bh = (long long)batch * heads;
   const long long wg256 = bh * ((seq_len + 255) / 256);
-  if (wg256 >= 512 || (!causal && wg256 >= 256)) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 2);
-  return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 3);
+  const long long wg128 = bh * ((seq_len + 127) / 128);
+  const long long nqb256 = (seq_len + 255) / 256;
+  if (seq_len <= 128) return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
+  // causal with about one 256-row item per CU: the snake cannot balance item
+  // costs 1..nqb256, so the KV-pair's halved heaviest key loop wins from
+  // nqb256 = 4 on (B=2 S=1024: 503 vs 461; B=4 S=512: 264 vs 364)
+  const bool persist = causal ? (wg256 >= 384 || (wg256 >= 256 && nqb256 <= 2)) : wg256 >= 256;
+  if (persist) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 2);
+  if (wg128 <= 512) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 3);
+  return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
 }
 
 namespace fa {
