@@ -5,15 +5,13 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py tests/test_persistent_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_parity.log 2>&1 || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py tests/test_persistent_gpu.py tests/test_kvpair_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_parity.log 2>&1 || exit 1
 cd flash-attention-cuda_amd
 #timeout -k 10 60 python tools/stamps.py --config 31 --seq 1024 --causal > ../gpurun_out/stamps.txt 2>&1
 timeout -k 10 60 python tools/stamps.py --config 15 --seq 4096 --batch 16 --causal > ../gpurun_out/stamps.txt 2>&1
 AB() { timeout -k 10 200 python tools/ab.py "$@" || exit 1; }
 {
-AB --configs 15 --libs ,nopre,head --seq 4096 --batch 64 --causal --rounds 5 --iters 5
-AB --configs 15 --libs ,nopre,head --seq 4096 --batch 16 --causal --rounds 7 --iters 10
-AB --configs 15 --libs ,nopre,head --seq 8192 --causal --rounds 7 --iters 20
-AB --configs 14 --libs ,nopre,head --seq 8192 --rounds 7 --iters 10
-AB --configs 14 --libs ,nopre,head --seq 4096 --batch 16 --rounds 7 --iters 10
+AB --configs 15 --libs ,q6p12,q2p8,q4p16 --seq 4096 --batch 16 --causal --rounds 7 --iters 10
+AB --configs 15 --libs ,q6p12,q2p8,q4p16 --seq 8192 --causal --rounds 7 --iters 20
+AB --configs 14 --libs ,q6p12,q2p8,q4p16 --seq 8192 --rounds 7 --iters 10
 } > ../gpurun_out/ab.jsonl 2>&1
