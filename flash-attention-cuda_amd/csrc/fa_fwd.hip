@@ -184,9 +184,25 @@ template <int BN, bool CAUSAL, bool BF16 = false, int HDIM = 128>
 __global__ __launch_bounds__(512, 2) void fa_fwd_f16_kvpair_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using Pol = M16<BN, typename std::conditional<BF16, __bf16, f16>::type, HDIM>;
+#ifdef FA_STAMPS
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long c_start = __builtin_amdgcn_s_memtime();
+#endif
   int qb, bh;
   map_block(blockIdx.x, gridDim.x, p.nqb, p.bh, p.band, CAUSAL, qb, bh);
   attention_kvpair<Pol, CAUSAL>(p, bh, qb, smem);
+#ifdef FA_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < FA_MAX_TIMELINE) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_fa_timeline[blockIdx.x][0] = t_start;
+    g_fa_timeline[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+    g_fa_timeline[blockIdx.x][3] = __builtin_amdgcn_s_memtime() - c_start;
+    g_fa_timeline[blockIdx.x][2] =
+        (unsigned long long)hw | ((unsigned long long)xcc << 32) | ((unsigned long long)qb << 40);
+  }
+#endif
 }
 
 // Split-KV: workgroup id -> (split, item); items ordered as map_block.

@@ -1232,7 +1232,7 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   const int n = (kv_hi + BN - 1) / BN;
 
 #ifdef FA_STAMPS
-  unsigned long long st_acc[11] = {}, sa, sb;
+  unsigned long long st_acc[12] = {}, sa, sb;
   const unsigned long long t_in = __builtin_amdgcn_s_memtime();
 #define FA_KSTAMP(v)                                                          \
   do {                                                                        \
@@ -1368,19 +1368,32 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
 #endif
 
   // merge: group B parks its partial state, group A combines and stores
+  // (FA_DIAG_NO_MERGE: diagnostic timing build only, group A stores its half
+  // unmerged -- the merge costs 2-7 % at B=1 H=32 S=512-2048)
+#ifndef FA_DIAG_NO_MERGE
   char* region = smem + rw * Pol::MERGE_BYTES;
   if (grp == 1) pol.put_partial(region);
   __syncthreads();
+#endif
+#ifdef FA_STAMPS
+  unsigned long long e1, e2;
+  FA_KSTAMP(e1);
+#endif
   if (grp == 0) {
+#ifndef FA_DIAG_NO_MERGE
     pol.merge_partial(region);
+#endif
     pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);
   }
 #ifdef FA_STAMPS
+  FA_KSTAMP(e2);
+  st_acc[5] = (e1 - t_le) * st_acc[6];   // printed per iteration: park + barrier
+  st_acc[11] = e2 - e1;                  // merge + store issue
   __builtin_amdgcn_s_waitcnt(0);
   st_acc[8] = __builtin_amdgcn_s_memtime() - t_le;
   st_acc[9] = 1;
   if (lane == 0 && blockIdx.x < 64)
-    for (int i = 0; i < 11; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
+    for (int i = 0; i < 12; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
 #endif
 #undef FA_KSTAMP
 }

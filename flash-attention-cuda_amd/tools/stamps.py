@@ -39,4 +39,5 @@ for w in range(8):
     vals = [buf[w * 12 + i] / iters for i in range(6)]
     print(w, " ".join(f"{x:9.0f}" for x in vals[:5]), f" total {sum(vals[:5]):.0f} |", f"{vals[5]:.0f}",
           f" iters {iters} | {buf[w * 12 + 7] / items:.0f} {buf[w * 12 + 8] / items:.0f}  items {items}"
-          f" | load-wait in lds_write {buf[w * 12 + 10] / iters:.0f}")
+          f" | load-wait in lds_write {buf[w * 12 + 10] / iters:.0f}"
+          f" | epi-pre-wait {buf[w * 12 + 11] / items:.0f}")
