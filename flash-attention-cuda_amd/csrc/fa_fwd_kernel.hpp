@@ -755,16 +755,13 @@ struct M16 {
   // lane-linearly (both waves hold the same query rows in the same lanes).
   // Region per wave: 2*NE f32x4 of O, then one f32x4 {m_0, l_0, m_1, l_1}.
   static constexpr int MERGE_BYTES = (2 * NE + 1) * 64 * 16;
-#ifdef FA_ROWSUM_VALU
-#error "KV-pair merge assumes MFMA row sums (lacc holds the full row sum)"
-#endif
   __device__ __forceinline__ void put_partial(char* region) const {
     f32x4* d = reinterpret_cast<f32x4*>(region);
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int e = 0; e < NE; ++e) d[(b * NE + e) * 64 + lane] = acc[b][e];
-    d[2 * NE * 64 + lane] = f32x4{m_ref[0], lacc[0][0], m_ref[1], lacc[1][0]};
+    d[2 * NE * 64 + lane] = f32x4{m_ref[0], row_sum(0), m_ref[1], row_sum(1)};
   }
   // O = O_a 2^(m_a-M) + O_b 2^(m_b-M), l likewise, M = max over partials that saw a key
   __device__ __forceinline__ void merge_partial(const char* region) {
@@ -772,7 +769,7 @@ struct M16 {
     const f32x4 ml = d[2 * NE * 64 + lane];
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
-      const float la = lacc[b][0], lb = ml[2 * b + 1];
+      const float la = row_sum(b), lb = ml[2 * b + 1];
       const float ma = la > 0.f ? m_ref[b] : ninf();
       const float mb = lb > 0.f ? ml[2 * b] : ninf();
       float M = fmaxf(ma, mb);
@@ -781,7 +778,11 @@ struct M16 {
 #pragma unroll
       for (int e = 0; e < NE; ++e) acc[b][e] = acc[b][e] * wa + d[(b * NE + e) * 64 + lane] * wb;
       const float l = la * wa + lb * wb;
+#ifdef FA_ROWSUM_VALU
+      lacc[b] = f32x4{g == 0 ? l : 0.f, 0.f, 0.f, 0.f};  // row_sum() adds the 4 lanes of a row
+#else
       lacc[b] = f32x4{l, l, l, l};
+#endif
       m_ref[b] = M;
     }
   }
