@@ -145,15 +145,35 @@ template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED, bool BF16 = f
 __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int x = blockIdx.x & 7, lcu = blockIdx.x >> 3, C = gridDim.x >> 3;
+  // head-affine XCD split when B*H % 8 == 0; otherwise heads do not divide
+  // over the 8 XCDs (B=1 H=2 would leave 6 of them idle: 343 vs 1000+
+  // TFLOP/s at S=32768), so XCD x takes every 8th item of the global list
+  // (causal: rank-major, heaviest first -- a balanced mix) or a contiguous
+  // 1/8 of it (non-causal: head-major, so runs of one head's query blocks)
+  const bool affine = (p.bh & 7) == 0;
+  const int Lall = p.bh * p.nqb;
   const int hx = (p.bh - x + 7) >> 3;  // heads h < bh with h % 8 == x
-  const int L = hx * p.nqb;
+  const int per8 = Lall >> 3, rem8 = Lall & 7;
+  const int L = affine ? hx * p.nqb : (CAUSAL ? (Lall - x + 7) >> 3 : per8 + (x < rem8 ? 1 : 0));
+  const int start8 = x * per8 + min(x, rem8);
   for (int r = 0; r * C < L; ++r) {
     const int pos = r * C + ((r & 1) ? (C - 1 - lcu) : lcu);
     if (pos < L) {
-      int lh, rank;
-      xcd_item(pos, hx, p.nqb, p.band, CAUSAL, lh, rank);
-      const int bh = x + 8 * lh;
-      const int qb = CAUSAL ? p.nqb - 1 - rank : rank;
+      int bh, qb;
+      if (affine) {
+        int lh, rank;
+        xcd_item(pos, hx, p.nqb, p.band, CAUSAL, lh, rank);
+        bh = x + 8 * lh;
+        qb = CAUSAL ? p.nqb - 1 - rank : rank;
+      } else if (CAUSAL) {
+        const int g = x + 8 * pos, rank = g / p.bh;
+        bh = g - rank * p.bh;
+        qb = p.nqb - 1 - rank;
+      } else {
+        const int g = start8 + pos;
+        bh = g / p.nqb;
+        qb = g - bh * p.nqb;
+      }
 #ifdef FA_STAMPS
       const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
       const unsigned long long c_start = __builtin_amdgcn_s_memtime();
@@ -407,7 +427,8 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   if (blocks > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
   if (cfg.kind == 2) {
     // one workgroup per CU, 8 per XCD group; never more than the items per XCD
-    const long long per_xcd = (long long)((bh + 7) / 8) * p.nqb;
+    const long long per_xcd = (bh & 7) == 0 ? (long long)(bh / 8) * p.nqb
+                                            : ((long long)bh * p.nqb + 7) / 8;
     const long long c = std::min<long long>(std::max(1, num_cus() / 8), per_xcd);
     blocks = 8 * c;
   }

@@ -11,9 +11,7 @@ cd flash-attention-cuda_amd
 timeout -k 10 60 python tools/stamps.py --config 15 --seq 4096 --batch 16 --causal > ../gpurun_out/stamps.txt 2>&1
 AB() { timeout -k 10 200 python tools/ab.py "$@" || exit 1; }
 {
-AB --configs 15 --libs ,rsvalu --seq 4096 --batch 16 --causal --rounds 7 --iters 10
-AB --configs 15 --libs ,rsvalu --seq 8192 --causal --rounds 7 --iters 20
-AB --configs 14 --libs ,rsvalu --seq 8192 --rounds 7 --iters 10
-AB --configs 31 --libs ,rsvalu --seq 1024 --causal --rounds 7 --iters 50
-AB --configs 30 --libs ,rsvalu --seq 1024 --rounds 7 --iters 50
+AB --configs 15 --seq 4096 --batch 16 --causal --rounds 5 --iters 10
+AB --configs 14 --seq 8192 --rounds 5 --iters 10
 } > ../gpurun_out/ab.jsonl 2>&1
+timeout -k 10 300 python tools/splitkv_study.py > ../gpurun_out/splitkv_study.jsonl 2>&1

@@ -56,6 +56,7 @@ SHAPES = [
     (1, 203, 300),   # odd head count, 2 query blocks, last one ragged
     (4, 50, 64),     # single-tile items (n = 1)
     (1, 7, 4096),    # fewer heads than XCD groups
+    (1, 2, 4096),    # 2 heads: non-affine split of the items over all 8 XCDs
 ]
 
 
