@@ -492,8 +492,9 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   // Tier table re-derived for 256 CUs (ref :620-661 picks by seq >= 2048 on
   // 58 SMs), from tools/small_s.py and tools/sweep.py on the box:
   //  * 8-wave persistent ping-pong (256 rows / workgroup) once there are
-  //    1.5 256-row items per CU, or one per CU without a mask (S=2048 B=1
-  //    H=32 non-causal: 1015 vs 873 TFLOP/s) or with short items;
+  //    1.5 256-row items per CU, or 0.6 per CU without a mask (S=2048 B=1
+  //    H=32 non-causal: 1015 vs 873 TFLOP/s), or one per CU of short items
+  //    (profiles/r01_tier_study.jsonl, r01_tier_study_heads.jsonl);
   //  * S <= 128: the 4-wave 128-row loop (a 256-row item would be half
   //    padding: B=64 H=32 S=128 364 vs 229 TFLOP/s non-causal);
   //  * under-filled launches (<= 512 128-row blocks): the KV-pair kernel
@@ -512,7 +513,9 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   // causal with about one 256-row item per CU: the snake cannot balance item
   // costs 1..nqb256, so the KV-pair's halved heaviest key loop wins from
   // nqb256 = 4 on (B=2 S=1024: 503 vs 461; B=4 S=512: 264 vs 364)
-  const bool persist = causal ? (wg256 >= 384 || (wg256 >= 256 && nqb256 <= 2)) : wg256 >= 256;
+  // non-causal: from 160 items (B=1 H=24 S=2048: 829 vs KV-pair 668; H=6
+  // S=8192: 1039 vs 854; at 128 items the KV-pair still wins, 732 vs 532)
+  const bool persist = causal ? (wg256 >= 384 || (wg256 >= 256 && nqb256 <= 2)) : wg256 >= 160;
   if (persist) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 2);
   if (wg128 <= 512) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 3);
   return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
