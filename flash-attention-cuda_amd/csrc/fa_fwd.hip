@@ -156,24 +156,38 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(Fw
   const int per8 = Lall >> 3, rem8 = Lall & 7;
   const int L = affine ? hx * p.nqb : (CAUSAL ? (Lall - x + 7) >> 3 : per8 + (x < rem8 ? 1 : 0));
   const int start8 = x * per8 + min(x, rem8);
-  for (int r = 0; r * C < L; ++r) {
+  auto item_of = [&](int pos, int& bh, int& qb) {
+    if (affine) {
+      int lh, rank;
+      xcd_item(pos, hx, p.nqb, p.band, CAUSAL, lh, rank);
+      bh = x + 8 * lh;
+      qb = CAUSAL ? p.nqb - 1 - rank : rank;
+    } else if (CAUSAL) {
+      const int g = x + 8 * pos, rank = g / p.bh;
+      bh = g - rank * p.bh;
+      qb = p.nqb - 1 - rank;
+    } else {
+      const int g = start8 + pos;
+      bh = g / p.nqb;
+      qb = g - bh * p.nqb;
+    }
+  };
+  // Non-causal tail: items cost the same, so a last round of `tail` <= C/2
+  // items would leave C - tail CUs idle (1.5 items per CU: 75 %).  Those
+  // items run instead as 2*tail 128-row KV-pair halves on 2*tail CUs.
+#ifdef FA_NO_TAIL_SPLIT
+  constexpr bool kTailSplit = false;
+#else
+  constexpr bool kTailSplit = !CAUSAL && SCHED == 1;
+#endif
+  const int full = L / C, tail = L - full * C;
+  const bool split_tail = kTailSplit && tail > 0 && 2 * tail <= C;
+  const int rounds = split_tail ? full : (L + C - 1) / C;
+  for (int r = 0; r < rounds; ++r) {
     const int pos = r * C + ((r & 1) ? (C - 1 - lcu) : lcu);
     if (pos < L) {
       int bh, qb;
-      if (affine) {
-        int lh, rank;
-        xcd_item(pos, hx, p.nqb, p.band, CAUSAL, lh, rank);
-        bh = x + 8 * lh;
-        qb = CAUSAL ? p.nqb - 1 - rank : rank;
-      } else if (CAUSAL) {
-        const int g = x + 8 * pos, rank = g / p.bh;
-        bh = g - rank * p.bh;
-        qb = p.nqb - 1 - rank;
-      } else {
-        const int g = start8 + pos;
-        bh = g / p.nqb;
-        qb = g - bh * p.nqb;
-      }
+      item_of(pos, bh, qb);
 #ifdef FA_STAMPS
       const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
       const unsigned long long c_start = __builtin_amdgcn_s_memtime();
@@ -194,6 +208,14 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(Fw
 #endif
     }
     __syncthreads();  // LDS images are reused by the next item
+  }
+  if constexpr (kTailSplit) {
+    if (split_tail && lcu < 2 * tail) {
+      using Pol = M16<BN, typename std::conditional<BF16, __bf16, f16>::type, HDIM>;
+      int bh, qb;
+      item_of(full * C + (lcu >> 1), bh, qb);
+      attention_kvpair<Pol, CAUSAL>(p, bh, 2 * qb + (lcu & 1), smem);  // 128-row half
+    }
   }
 }
 
@@ -295,8 +317,11 @@ constexpr kernel_fn pick_kernel() {
 // DT: 0 = fp16, 1 = bf16 (FA_DTYPE_*)
 // LDS images keep 256-B row slots at head_dim 64 too (fa_fwd_kernel.hpp M16)
 #define FA_CFG_TD(ID, W, BN_, C, KIND, M, SCHED, DT, HDIM, NAME)                           \
-  {{ID, 32 * (W), BN_, W, C, (KIND) == 1, ((SCHED) == 3 ? 6 : 4) * (BN_) * ROW_BYTES, NAME, DT,  \
-    HDIM}, M, SCHED,                                                                        \
+  {{ID, 32 * (W), BN_, W, C, (KIND) == 1,                                                    \
+    ((SCHED) == 3 ? 6 * (BN_) * ROW_BYTES                                                   \
+     : ((KIND) == 2 && !(C)) ? std::max(4 * (BN_) * ROW_BYTES, kKvpairLdsBytes) /* tail */ \
+                   : 4 * (BN_) * ROW_BYTES),                                                \
+    NAME, DT, HDIM}, M, SCHED,                                                              \
    KIND, pick_kernel<W, BN_, C, KIND, M, SCHED, DT, HDIM>()}
 #define FA_CFG_T(ID, W, BN_, C, KIND, M, SCHED, DT, NAME) \
   FA_CFG_TD(ID, W, BN_, C, KIND, M, SCHED, DT, 128, NAME)

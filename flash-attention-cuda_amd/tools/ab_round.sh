@@ -11,7 +11,9 @@ cd flash-attention-cuda_amd
 timeout -k 10 60 python tools/stamps.py --config 15 --seq 4096 --batch 16 --causal > ../gpurun_out/stamps.txt 2>&1
 AB() { timeout -k 10 200 python tools/ab.py "$@" || exit 1; }
 {
-AB --configs 15 --seq 4096 --batch 16 --causal --rounds 5 --iters 10
-AB --configs 14 --seq 8192 --rounds 5 --iters 10
+AB --configs 14 --libs ,notail --heads 12 --seq 8192 --rounds 5 --iters 10
+AB --configs 14 --libs ,notail --heads 48 --seq 2048 --rounds 5 --iters 20
+AB --configs 14 --libs ,notail --heads 24 --seq 4096 --rounds 5 --iters 10
+AB --configs 14 --libs ,notail --seq 8192 --rounds 5 --iters 10
+AB --configs 15 --libs ,notail --seq 4096 --batch 16 --causal --rounds 5 --iters 10
 } > ../gpurun_out/ab.jsonl 2>&1
-timeout -k 10 300 python tools/splitkv_study.py > ../gpurun_out/splitkv_study.jsonl 2>&1
