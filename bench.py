@@ -315,7 +315,7 @@ def main():
             "frac": round(achieved / peak, 4),
             "traffic": traffic,
             "kernel": ("fa_fwd_f16_persistent_kernel" if "persistent" in cfg_name
-                       else "fa_fwd_f16_kvpair_kernel" if "kvpair" in cfg_name
+                       else "fa_fwd_f16_kvpair_kernel" if ("kvpair" in cfg_name or "kvquad" in cfg_name)
                        else "fa_fwd_f16_kernel") + f" ({cfg_name})",
             "avg_launch_ms": round(avg_launch_ms, 4),
             "flops_per_launch": flops_per_launch,

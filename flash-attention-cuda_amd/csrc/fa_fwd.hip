@@ -222,7 +222,8 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(Fw
 // KV-pair (short sequences): 128 query rows per workgroup, the two waves of a
 // SIMD split the key range (attention_kvpair); one workgroup per item, items
 // ordered as map_block.
-template <int BN, bool CAUSAL, bool BF16 = false, int HDIM = 128>
+// SUB = 2: KV-quad (64 query rows, four-way key split).
+template <int BN, bool CAUSAL, bool BF16 = false, int HDIM = 128, int SUB = 1>
 __global__ __launch_bounds__(512, 2) void fa_fwd_f16_kvpair_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using Pol = M16<BN, typename std::conditional<BF16, __bf16, f16>::type, HDIM>;
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(512, 2) void fa_fwd_f16_kvpair_kernel(FwdParams p) 
 #endif
   int qb, bh;
   map_block(blockIdx.x, gridDim.x, p.nqb, p.bh, p.band, CAUSAL, qb, bh);
-  attention_kvpair<Pol, CAUSAL>(p, bh, qb, smem);
+  attention_kvpair<Pol, CAUSAL, SUB>(p, bh, qb, smem);
 #ifdef FA_STAMPS
   if (threadIdx.x == 0 && blockIdx.x < FA_MAX_TIMELINE) {
     unsigned hw, xcc;
@@ -297,7 +298,8 @@ struct Config {
   fa_config_info_t info;
   int mfma;   // 32 = v_mfma_f32_32x32x16_f16 loop, 16 = v_mfma_f32_16x16x32_f16 loop
   int sched;  // 0 = one barrier per tile, 1 = 8-wave ping-pong
-  int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent, 3 = KV-pair
+  int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent, 3 = KV-pair,
+              // 4 = KV-quad
   kernel_fn fn;
 };
 
@@ -305,6 +307,8 @@ template <int W, int BN_, int C, int SPL, int M, int SCHED, int DT, int HDIM>
 constexpr kernel_fn pick_kernel() {
   if constexpr (SPL == 3)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
+  else if constexpr (SPL == 4)
+    return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM, 2>;
   else if constexpr (SPL == 1)
     return fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
   else if constexpr (SPL == 2)
@@ -330,6 +334,10 @@ constexpr kernel_fn pick_kernel() {
 #define FA_CFG_KVPAIR(ID, C, DT, HDIM, NAME)                                           \
   {{ID, 128, 64, 8, C, 0, kKvpairLdsBytes, NAME, DT, HDIM}, 16, 1, 3,                   \
    pick_kernel<8, 64, C, 3, 16, 1, DT, HDIM>()}
+// KV-quad: 8 waves on 64 query rows (four waves per row block, key range split four ways)
+#define FA_CFG_KVQUAD(ID, C, DT, HDIM, NAME)                                           \
+  {{ID, 64, 64, 8, C, 0, kKvquadLdsBytes, NAME, DT, HDIM}, 16, 1, 4,                    \
+   pick_kernel<8, 64, C, 4, 16, 1, DT, HDIM>()}
 
 static const Config kConfigs[] = {
     FA_CFG(0, 4, 64, 0, 0, 32, 0, "bm128_bn64_w4_m32_noncausal"),
@@ -375,6 +383,15 @@ static const Config kConfigs[] = {
     FA_CFG_KVPAIR(35, 1, 0, 64, "d64_bm128_bn64_w8_m16_kvpair_causal"),
     FA_CFG_KVPAIR(36, 0, 1, 64, "bf16_d64_bm128_bn64_w8_m16_kvpair_noncausal"),
     FA_CFG_KVPAIR(37, 1, 1, 64, "bf16_d64_bm128_bn64_w8_m16_kvpair_causal"),
+    // KV-quad (shortest sequences): four waves split the keys of 32 query rows
+    FA_CFG_KVQUAD(38, 0, 0, 128, "bm64_bn64_w8_m16_kvquad_noncausal"),
+    FA_CFG_KVQUAD(39, 1, 0, 128, "bm64_bn64_w8_m16_kvquad_causal"),
+    FA_CFG_KVQUAD(40, 0, 1, 128, "bf16_bm64_bn64_w8_m16_kvquad_noncausal"),
+    FA_CFG_KVQUAD(41, 1, 1, 128, "bf16_bm64_bn64_w8_m16_kvquad_causal"),
+    FA_CFG_KVQUAD(42, 0, 0, 64, "d64_bm64_bn64_w8_m16_kvquad_noncausal"),
+    FA_CFG_KVQUAD(43, 1, 0, 64, "d64_bm64_bn64_w8_m16_kvquad_causal"),
+    FA_CFG_KVQUAD(44, 0, 1, 64, "bf16_d64_bm64_bn64_w8_m16_kvquad_noncausal"),
+    FA_CFG_KVQUAD(45, 1, 1, 64, "bf16_d64_bm64_bn64_w8_m16_kvquad_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -527,12 +544,19 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   //    twice the workgroups of the 256-row tier and half the heaviest causal
   //    key loop; 1.0-1.2x the 4-wave loop at B=1 H=32, S=512-2048
   //    (profiles/r01_short_s_ab.jsonl);
+  //  * launches of <= 256 64-row blocks (one workgroup per CU): the KV-quad
+  //    (64 rows, four-way key split): B=1 H=8 S=2048 633 vs KV-pair 511,
+  //    H=4 S=4096 causal 396 vs 285; at 512 blocks it loses (H=16 S=2048
+  //    637 vs 907) (profiles/r01_kvquad_study.jsonl);
+  //  * S <= 256 short of the persistent tier: the 4-wave loop (B=1 H=32
+  //    S=256 109 vs KV-pair 100, B=4 387 vs 352, same study);
   //  * otherwise the 4-wave loop (with many blocks the KV-pair's doubled LDS
   //    traffic per FLOP costs more than its balance gains: B=16 S=512
   //    causal 4-wave 398 vs KV-pair 294, profiles/r01_tier_study.jsonl).
   const long long bh = (long long)batch * heads;
   const long long wg256 = bh * ((seq_len + 255) / 256);
   const long long wg128 = bh * ((seq_len + 127) / 128);
+  const long long wg64 = bh * ((seq_len + 63) / 64);
   const long long nqb256 = (seq_len + 255) / 256;
   if (seq_len <= 128) return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
   // causal with about one 256-row item per CU: the snake cannot balance item
@@ -542,6 +566,8 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   // S=8192: 1039 vs 854; at 128 items the KV-pair still wins, 732 vs 532)
   const bool persist = causal ? (wg256 >= 384 || (wg256 >= 256 && nqb256 <= 2)) : wg256 >= 160;
   if (persist) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 2);
+  if (seq_len <= 256) return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
+  if (wg64 <= 256) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 4);
   if (wg128 <= 512) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 3);
   return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
 }

@@ -56,6 +56,8 @@ constexpr int ROW_BYTES = HD * 2;  // one K/V/Q row in bytes
 constexpr float RESCALE_LOG2 = 8.0f;
 // attention_kvpair: 4 tile buffers (64 KB) or the merge region (4 x 17 KB at head_dim 128)
 constexpr int kKvpairLdsBytes = 4 * (2 * 8 + 1) * 64 * 16;
+// KV-quad: four double-width (128-key) stage buffers
+constexpr int kKvquadLdsBytes = 4 * 2 * 64 * 256;
 
 struct FwdParams {
   const f16* q;
@@ -82,6 +84,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, in
 }
 __device__ __forceinline__ f16x8 buf_load16(__amdgpu_buffer_rsrc_t r, int voff) {
   return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+}
+// row offset in the scalar soffset operand: one address VGPR for all passes
+__device__ __forceinline__ f16x8 buf_load16s(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 __device__ __forceinline__ void buf_store8(__amdgpu_buffer_rsrc_t r, int voff, f16x4 v) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, 0, 0);
@@ -1202,24 +1208,46 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
 // the start of its phase (-1.5 %, the softmax side is already the long pole);
 // one staging set, loads one half-step ahead (equal).
 // ---------------------------------------------------------------------------
-template <class Pol, bool CAUSAL>
+//
+// KV-quad (SUB = 2): 64 query rows per workgroup, four waves per 32 rows.  A
+// half-step stage is a 128-key super-tile (two 64-key images back to back);
+// in its MFMA half-step a group's waves 0-1 take the first image and waves
+// 2-3 the second, so wave w sees key tiles 2h + ((w & 3) >> 1) of the
+// half-steps h of its group: a four-way key split merged through LDS.  Twice
+// the workgroups of the KV-pair and half its per-wave key loop, for launches
+// that leave CUs idle even at 128 rows (B=1 H=32 S=512: 128 KV-pair
+// workgroups on 256 CUs).  One staging set (loads one half-step ahead): two
+// sets of the double-width stage would not fit the 256 VGPRs.
+template <class Pol, bool CAUSAL, int SUB = 1>
 __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int qb, char* smem) {
+  static_assert(SUB == 1 || SUB == 2, "key split 2 (KV-pair) or 4 (KV-quad)");
   constexpr int WAVES = 8;
   constexpr int BN = Pol::BN;
   constexpr int NT = WAVES * 64;
-  constexpr int BM = 128;
+  constexpr int RW = 4 / SUB;       // row waves per group (32 query rows each)
+  constexpr int BM = 32 * RW;       // 128 (KV-pair) or 64 (KV-quad)
+  constexpr int NP = 2 * SUB;       // partial states per query row (key splits)
+  constexpr int SBN = SUB * BN;     // keys per stage
   constexpr int HD = Pol::HDIM;
   constexpr int ROW_BYTES = 2 * HD;
   constexpr int TILE_BYTES = BN * 256;
-  constexpr int NCH = (BN * (HD / 8)) / NT;
-  static_assert((BN * (HD / 8)) % NT == 0, "tile chunks must divide evenly");
-  static_assert(4 * Pol::MERGE_BYTES <= kKvpairLdsBytes, "merge region fits the LDS allocation");
+  constexpr int STAGE_BYTES = SUB * TILE_BYTES;
+  constexpr int NCH = (SBN * (HD / 8)) / NT;
+  constexpr bool TWO_SETS = SUB == 1;
+  constexpr int NSET = TWO_SETS ? 2 : 1;
+  static_assert((SBN * (HD / 8)) % NT == 0, "tile chunks must divide evenly");
+  static_assert((NP - 1) * RW * Pol::MERGE_BYTES <= (SUB == 1 ? kKvpairLdsBytes : kKvquadLdsBytes),
+                "merge region fits the LDS allocation");
+  static_assert(4 * STAGE_BYTES <= (SUB == 1 ? kKvpairLdsBytes : kKvquadLdsBytes),
+                "stage buffers fit the LDS allocation");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wave >> 2;  // 0 = A (even tiles), 1 = B (odd tiles)
-  const int rw = wave & 3;    // row wave: both groups hold rows q0 + 32 rw ...
+  const int grp = wave >> 2;          // 0 = A (even half-steps), 1 = B (odd)
+  const int rw = wave & (RW - 1);     // row wave: rows q0 + 32 rw ...
+  const int sub = (wave & 3) / RW;    // image of the stage this wave consumes
+  const int pidx = wave / RW;         // partial index; 0 merges and stores
   const int S = p.seq_len;
 
   const size_t head_off = (size_t)bh * (size_t)S * HD;
@@ -1230,7 +1258,8 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   const int q0 = qb * BM;
   const int qw = q0 + rw * 32;
   const int kv_hi = CAUSAL ? min(q0 + BM, S) : S;
-  const int n = (kv_hi + BN - 1) / BN;
+  const int nt = (kv_hi + BN - 1) / BN;    // 64-key tiles
+  const int n = (kv_hi + SBN - 1) / SBN;   // stages
 
 #ifdef FA_STAMPS
   unsigned long long st_acc[12] = {}, sa, sb;
@@ -1251,25 +1280,33 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   pol.init(lane, p.c);
   pol.issue_q(make_rsrc(Qh, S * ROW_BYTES), qw);
 
-  auto kbuf = [&](int x) { return smem + (x & 1) * TILE_BYTES; };
-  auto vbuf = [&](int x) { return smem + (2 + (x & 1)) * TILE_BYTES; };
+  auto kbuf = [&](int x) { return smem + (x & 1) * STAGE_BYTES; };
+  auto vbuf = [&](int x) { return smem + (2 + (x & 1)) * STAGE_BYTES; };
   const int kr0 = pol.k_stage_row(wave), kc = pol.k_stage_ch();
   const int vr0 = pol.v_stage_row(wave), vc = pol.v_stage_ch();
-  // staging set 0 carries the stages of this wave's MFMA half-steps, set 1
-  // those of its softmax half-steps (they alternate)
-  f16x8 kst[2][NCH], vst[2][NCH];
+  // two sets: set 0 carries the stages of this wave's MFMA half-steps, set 1
+  // those of its softmax half-steps (they alternate); one set: every stage
+  f16x8 kst[NSET][NCH], vst[NSET][NCH];
   // loads of stage h = (K_{h+1}, V_{h-1}); rows at/after kv_hi, and tiles
   // outside [0, n), read as 0 with no memory traffic
   auto issue_stage = [&](int h, auto set_c) {
     constexpr int X = decltype(set_c)::value;
-    const int kb_row = (h + 1) * BN, vb_row = (h - 1) * BN;
+    const int kb_row = (h + 1) * SBN, vb_row = (h - 1) * SBN;
     const auto rk = make_rsrc(Kh + (size_t)min(kb_row, S) * HD, (kv_hi - kb_row) * ROW_BYTES);
     const auto rv = make_rsrc(Vh + (size_t)max(vb_row, 0) * HD,
                               vb_row < 0 ? 0 : (kv_hi - vb_row) * ROW_BYTES);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      kst[X][i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
-      vst[X][i] = buf_load16(rv, (vr0 + Pol::RPW * WAVES * i) * ROW_BYTES + vc * 16);
+      // KV-quad: per-pass row offsets in the scalar soffset (with four
+      // passes in VGPRs the kernel spilled); KV-pair: in VGPRs (+1-4 % A/B,
+      // profiles/r01_ab_kvpair_soffset.jsonl)
+      if constexpr (SUB == 1) {
+        kst[X][i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
+        vst[X][i] = buf_load16(rv, (vr0 + Pol::RPW * WAVES * i) * ROW_BYTES + vc * 16);
+      } else {
+        kst[X][i] = buf_load16s(rk, kr0 * ROW_BYTES + kc * 16, Pol::RPW * WAVES * i * ROW_BYTES);
+        vst[X][i] = buf_load16s(rv, vr0 * ROW_BYTES + vc * 16, Pol::RPW * WAVES * i * ROW_BYTES);
+      }
     }
   };
   auto write_stage = [&](int h, auto set_c) {
@@ -1296,8 +1333,12 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
     // first softmax one (A: h=1, B: the idle h=0); branch-free: a per-group
     // branch makes hipcc merge the paths with register copies that wait for
     // the loads
-    issue_stage(grp, Set0{});
-    issue_stage(1 - grp, Set1{});
+    if constexpr (TWO_SETS) {
+      issue_stage(grp, Set0{});
+      issue_stage(1 - grp, Set1{});
+    } else {
+      issue_stage(0, Set0{});
+    }
     __builtin_amdgcn_sched_barrier(0);  // all prologue loads issued first (attention_tile_loop)
     pol.scale_q();
 #pragma unroll
@@ -1305,24 +1346,29 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
       *reinterpret_cast<f16x8*>(kbuf(0) + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = k0[i];
   }
   // Q and K_0 retired (see attention_tile_loop); the stage loads may stay in flight
-  __builtin_amdgcn_s_waitcnt(0x0F70 | (4 * NCH));
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * NSET * NCH));
   __syncthreads();
 #ifdef FA_STAMPS
   st_acc[7] = __builtin_amdgcn_s_memtime() - t_in;
 #endif
 
   const float c = p.c;
-  auto active = [&](int t) { return t >= 0 && t < n && (!CAUSAL || t * BN <= qw + 31); };
+  // this wave's key tile of stage h is t = SUB h + sub
+  auto active = [&](int h) {
+    const int t = SUB * h + sub;
+    return h >= 0 && t < nt && (!CAUSAL || t * BN <= qw + 31);
+  };
   // end of half-step h: publish its stage, refill the staging set, barrier
   auto half_step_end = [&](int h, auto set_c, int bar_slot) {
 #ifdef FA_STAMPS
     unsigned long long w0, w1, w2, w3;
     FA_KSTAMP(w0);
-    __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * NCH));
+    __builtin_amdgcn_s_waitcnt(0x0F70 | (TWO_SETS ? 2 * NCH : 0));
     FA_KSTAMP(w1);
 #endif
-    write_stage(h, set_c);
-    issue_stage(h + 2, set_c);
+    using SetX = std::integral_constant<int, TWO_SETS ? decltype(set_c)::value : 0>;
+    write_stage(h, SetX{});
+    issue_stage(h + NSET, SetX{});
 #ifdef FA_STAMPS
     FA_KSTAMP(w2);
 #endif
@@ -1342,7 +1388,8 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
     const int h = 2 * m + grp;
     FA_KSTAMP(sa);
     __builtin_amdgcn_s_setprio(1);
-    pol.mfma_block(kbuf(h), vbuf(h - 2), active(h - 2), active(h));
+    pol.mfma_block(kbuf(h) + sub * TILE_BYTES, vbuf(h - 2) + sub * TILE_BYTES, active(h - 2),
+                   active(h));
     __builtin_amdgcn_s_setprio(0);
     FA_KSTAMP(sb);
 #ifdef FA_STAMPS
@@ -1351,7 +1398,7 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
     half_step_end(h, Set0{}, 1);
     FA_KSTAMP(sa);
     if (active(h)) {
-      const int kv0 = h * BN;
+      const int kv0 = (SUB * h + sub) * BN;
       const bool need_mask = (kv0 + BN > kv_hi) || (CAUSAL && kv0 + BN - 1 > qw);
       pol.template softmax<CAUSAL>(kv0, kv_hi, qw, c, need_mask);
     }
@@ -1372,17 +1419,18 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   // (FA_DIAG_NO_MERGE: diagnostic timing build only, group A stores its half
   // unmerged -- the merge costs 2-7 % at B=1 H=32 S=512-2048)
 #ifndef FA_DIAG_NO_MERGE
-  char* region = smem + rw * Pol::MERGE_BYTES;
-  if (grp == 1) pol.put_partial(region);
+  // partial j >= 1 of row wave rw parks in slot (j - 1) RW + rw
+  if (pidx > 0) pol.put_partial(smem + ((pidx - 1) * RW + rw) * Pol::MERGE_BYTES);
   __syncthreads();
 #endif
 #ifdef FA_STAMPS
   unsigned long long e1, e2;
   FA_KSTAMP(e1);
 #endif
-  if (grp == 0) {
+  if (pidx == 0) {
 #ifndef FA_DIAG_NO_MERGE
-    pol.merge_partial(region);
+#pragma unroll
+    for (int j = 1; j < NP; ++j) pol.merge_partial(smem + ((j - 1) * RW + rw) * Pol::MERGE_BYTES);
 #endif
     pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);
   }

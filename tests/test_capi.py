@@ -73,6 +73,11 @@ def test_config_table():
             assert c.block_m == 16 * c.waves
             assert c.lds_bytes == max(4 * c.block_n * 256, 4 * 17 * 64 * 16)
             continue
+        if "_kvquad_" in c.name:
+            # four waves per 32 query rows; four double-width stage buffers
+            assert c.block_m == 8 * c.waves
+            assert c.lds_bytes == 4 * 2 * c.block_n * 256
+            continue
         assert c.block_m == 32 * c.waves
         # K and V image buffers of 256-B row slots: double-buffered, or three
         # rotating buffers each for the LDS-DMA configs
@@ -100,6 +105,10 @@ def test_select_config(causal):
     # the long ones to the 256-row persistent ping-pong
     assert "_kvpair_" in cfgs[fa.select_config(1, 32, 1024, causal)].name
     assert "_persistent_" in cfgs[fa.select_config(1, 32, 8192, causal)].name
+    # launches of <= 256 64-row blocks: the KV-quad; S=256: the 4-wave loop
+    assert "_kvquad_" in cfgs[fa.select_config(1, 8, 2048, causal)].name
+    assert "_kvquad_" in cfgs[fa.select_config(1, 32, 512, causal)].name
+    assert "_w4_" in cfgs[fa.select_config(1, 32, 256, causal)].name
 
 
 def _null_call(lib, head_dim=128, b=1, h=1, s=64, causal=0, ptr=None):
