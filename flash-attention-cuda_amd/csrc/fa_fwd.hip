@@ -140,23 +140,25 @@ __device__ __forceinline__ void xcd_item(int j, int hx, int nqb, int band, bool 
   }
 }
 
-template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED, bool BF16 = false,
-          int HDIM = 128>
-__global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(FwdParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int x = blockIdx.x & 7, lcu = blockIdx.x >> 3, C = gridDim.x >> 3;
-  // head-affine XCD split when B*H % 8 == 0; otherwise heads do not divide
-  // over the 8 XCDs (B=1 H=2 would leave 6 of them idle: 343 vs 1000+
-  // TFLOP/s at S=32768), so XCD x takes every 8th item of the global list
-  // (causal: rank-major, heaviest first -- a balanced mix) or a contiguous
-  // 1/8 of it (non-causal: head-major, so runs of one head's query blocks)
-  const bool affine = (p.bh & 7) == 0;
-  const int Lall = p.bh * p.nqb;
-  const int hx = (p.bh - x + 7) >> 3;  // heads h < bh with h % 8 == x
-  const int per8 = Lall >> 3, rem8 = Lall & 7;
-  const int L = affine ? hx * p.nqb : (CAUSAL ? (Lall - x + 7) >> 3 : per8 + (x < rem8 ? 1 : 0));
-  const int start8 = x * per8 + min(x, rem8);
-  auto item_of = [&](int pos, int& bh, int& qb) {
+// The item list of XCD x (blockIdx & 7) for the persistent kernels.
+// Head-affine XCD split when B*H % 8 == 0; otherwise heads do not divide
+// over the 8 XCDs (B=1 H=2 would leave 6 of them idle: 343 vs 1000+
+// TFLOP/s at S=32768), so XCD x takes every 8th item of the global list
+// (causal: rank-major, heaviest first -- a balanced mix) or a contiguous
+// 1/8 of it (non-causal: head-major, so runs of one head's query blocks).
+template <bool CAUSAL>
+struct XcdItems {
+  int x, hx, start8, L;
+  bool affine;
+  __device__ __forceinline__ XcdItems(const FwdParams& p, int x_) : x(x_) {
+    affine = (p.bh & 7) == 0;
+    const int Lall = p.bh * p.nqb;
+    hx = (p.bh - x + 7) >> 3;  // heads h < bh with h % 8 == x
+    const int per8 = Lall >> 3, rem8 = Lall & 7;
+    L = affine ? hx * p.nqb : (CAUSAL ? (Lall - x + 7) >> 3 : per8 + (x < rem8 ? 1 : 0));
+    start8 = x * per8 + min(x, rem8);
+  }
+  __device__ __forceinline__ void item(const FwdParams& p, int pos, int& bh, int& qb) const {
     if (affine) {
       int lh, rank;
       xcd_item(pos, hx, p.nqb, p.band, CAUSAL, lh, rank);
@@ -171,7 +173,17 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(Fw
       bh = g / p.nqb;
       qb = g - bh * p.nqb;
     }
-  };
+  }
+};
+
+template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED, bool BF16 = false,
+          int HDIM = 128>
+__global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(FwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int x = blockIdx.x & 7, lcu = blockIdx.x >> 3, C = gridDim.x >> 3;
+  const XcdItems<CAUSAL> items(p, x);
+  const int L = items.L;
+  auto item_of = [&](int pos, int& bh, int& qb) { items.item(p, pos, bh, qb); };
   // Non-causal tail: items cost the same, so a last round of `tail` <= C/2
   // items would leave C - tail CUs idle (1.5 items per CU: 75 %).  Those
   // items run instead as 2*tail 128-row KV-pair halves on 2*tail CUs.
@@ -309,6 +321,7 @@ constexpr kernel_fn pick_kernel() {
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
   else if constexpr (SPL == 4)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM, 2>;
+
   else if constexpr (SPL == 1)
     return fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
   else if constexpr (SPL == 2)

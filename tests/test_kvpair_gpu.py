@@ -123,3 +123,4 @@ def test_kvpair_twins_vs_fp32(dtype, head_dim, kind):
                                                                is_causal=causal)
         tol = 5e-3 if dtype == "bfloat16" else 1e-3
         assert (o.float() - ref).abs().max().item() <= tol
+
