@@ -1,0 +1,150 @@
+"""Per-tier MFMA utilisation and HBM traffic table (north_star: "rocprof reports
+achieved MFMA utilisation and HBM GB/s against the chip's fp16 peak for each
+(BM,BN,warps) tile config").
+
+One process walks a fixed list of shapes, each on the tier the dispatcher
+picks for it, ITERS launches per shape, in a fixed order -- so the n-th fa::
+dispatch of a rocprofv3 pass maps back to its shape.
+
+  python tools/tier_pmc.py run [--time]      # the workload (under rocprofv3, or --time: HIP events)
+  python tools/tier_pmc.py summary T.jsonl MFMA_DIR FETCH_DIR WRITE_DIR OUT.jsonl
+
+Counter passes (separate runs, MI355X_MICROARCH.md §rocprofv3 PMC slots):
+  --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE
+  --pmc FETCH_SIZE          (x1024 B, x2: gfx950 half-counts wide reads)
+  --pmc WRITE_SIZE          (x1024 B)
+Derived per launch (first launch of each shape dropped):
+  mfma_busy   = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)
+                -- fraction of SIMD-cycles the matrix pipe was busy, at whatever
+                clock the chip held (the guide's DVFS note)
+  eff_clock   = GRBM_GUI_ACTIVE / 8 / profiled kernel time
+  frac_nominal = TFLOP/s (un-profiled, HIP events) / 2516.6
+  hbm_gbs     = (FETCH + WRITE bytes) / un-profiled time
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+SHAPES = [  # (label, batch, heads, seq, causal)
+    ("cfg0_s512_noncausal", 1, 32, 512, False),
+    ("cfg1_s1024_causal", 1, 32, 1024, True),
+    ("s1024_noncausal", 1, 32, 1024, False),
+    ("s2048_causal", 1, 32, 2048, True),
+    ("s4096_noncausal", 1, 32, 4096, False),
+    ("cfg2_s8192_noncausal", 1, 32, 8192, False),
+    ("target_s8192_causal", 1, 32, 8192, True),
+    ("cfg3_s16384_causal", 1, 32, 16384, True),
+    ("cfg4_b8_s4096_causal_shard", 8, 32, 4096, True),   # one GPU's shard of config 5 at N=8
+    ("headline_b64_s4096_causal", 64, 32, 4096, True),
+    ("s256_b16_noncausal", 16, 32, 256, False),
+]
+ITERS = 6
+PEAK = 2516.6  # TFLOP/s, 256 CU x 2.4 GHz x 4096 FLOP/clk/CU
+SIMDS = 1024
+XCDS = 8
+KERNEL_TAG = "fa::"
+
+
+def run(time_it):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import fa_mi355x as fa
+
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    for label, b, h, s, causal in SHAPES:
+        shape = (b, h, s, 128)
+        q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5, generator=g)
+                   for _ in range(3))
+        o = torch.empty_like(q)
+        cfg = fa.select_config(b, h, s, causal)
+        flops = fa.attention_flops(b, h, s, 128, causal)
+        torch.cuda.synchronize()
+        if time_it:
+            for _ in range(3):
+                fa.flash_attention_fwd(q, k, v, causal, out=o)
+            n = 50 if flops < 1e12 else 10
+            best = []
+            for _ in range(3):
+                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                st.record()
+                for _ in range(n):
+                    fa.flash_attention_fwd(q, k, v, causal, out=o)
+                en.record()
+                en.synchronize()
+                best.append(st.elapsed_time(en) / n)
+            ms = sorted(best)[1]
+            print(json.dumps({"label": label, "batch": b, "heads": h, "seq": s, "causal": causal,
+                              "config": fa.configs()[cfg].name, "ms": ms,
+                              "tflops": flops / (ms / 1e3) / 1e12, "flops": flops,
+                              "alg_bytes": 8.0 * b * h * s * 128}), flush=True)
+        else:
+            for _ in range(ITERS):
+                fa.flash_attention_fwd(q, k, v, causal, out=o)
+            torch.cuda.synchronize()
+        del q, k, v, o
+
+
+def per_dispatch(root, names):
+    """{counter: [value per fa:: dispatch, in dispatch order]} and kernel ns per dispatch."""
+    files = glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {root}")
+    per, dur, kname = {}, {}, {}
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if KERNEL_TAG not in r["Kernel_Name"] or r["Counter_Name"] not in names:
+                continue
+            d = int(r["Dispatch_Id"])
+            per.setdefault(r["Counter_Name"], {}).setdefault(d, 0.0)
+            per[r["Counter_Name"]][d] += float(r["Counter_Value"])
+            dur[d] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            kname[d] = r["Kernel_Name"]
+    order = sorted(dur)
+    return {n: [per[n][d] for d in order] for n in per}, [dur[d] for d in order], [kname[d] for d in order]
+
+
+def summary(timing_jsonl, mfma_dir, fetch_dir, write_dir, out):
+    timing = {json.loads(l)["label"]: json.loads(l) for l in open(timing_jsonl) if l.startswith("{")}
+    m, dur, kn = per_dispatch(mfma_dir, {"SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_MFMA", "GRBM_GUI_ACTIVE"})
+    f, _, _ = per_dispatch(fetch_dir, {"FETCH_SIZE"})
+    w, _, _ = per_dispatch(write_dir, {"WRITE_SIZE"})
+    # a launch may be one kernel (all dispatched tiers are single-kernel)
+    assert len(dur) == ITERS * len(SHAPES), (len(dur), ITERS * len(SHAPES))
+    rows = []
+    for i, (label, b, h, s, causal) in enumerate(SHAPES):
+        sl = slice(i * ITERS + 1, (i + 1) * ITERS)  # drop the first (cold) launch
+        mean = lambda xs: sum(xs[sl]) / len(xs[sl])
+        busy, grbm, nmf = mean(m["SQ_VALU_MFMA_BUSY_CYCLES"]), mean(m["GRBM_GUI_ACTIVE"]), mean(m["SQ_INSTS_MFMA"])
+        hbm = mean(f["FETCH_SIZE"]) * 1024 * 2 + mean(w["WRITE_SIZE"]) * 1024
+        t = timing[label]
+        rows.append({
+            "label": label, "config": t["config"], "kernel": kn[i * ITERS].split("(")[0],
+            "batch": b, "heads": h, "seq": s, "causal": causal,
+            "ms": round(t["ms"], 4), "tflops": round(t["tflops"], 1),
+            "frac_nominal_peak": round(t["tflops"] / PEAK, 4),
+            "mfma_busy": round(busy / (SIMDS * grbm / XCDS), 4),
+            "mfma_insts": nmf, "busy_cycles_per_mfma": round(busy / nmf, 2),
+            "eff_clock_ghz_profiled": round(grbm / XCDS / mean(dur), 3),
+            "hbm_bytes": int(hbm), "alg_bytes": int(t["alg_bytes"]),
+            "traffic_over_alg": round(hbm / t["alg_bytes"], 3),
+            "hbm_gbs": round(hbm / (t["ms"] / 1e3) / 1e9, 1),
+            "hbm_frac_8tbs": round(hbm / (t["ms"] / 1e3) / 8e12, 4),
+        })
+    with open(out, "w") as fo:
+        for r in rows:
+            fo.write(json.dumps(r) + "\n")
+    hdr = f"{'shape':30s} {'tier':50s} {'TF/s':>7s} {'%peak':>6s} {'mfma':>6s} {'GHz':>5s} {'GB/s':>7s} {'tr/alg':>6s}"
+    print(hdr)
+    for r in rows:
+        print(f"{r['label']:30s} {r['config']:50s} {r['tflops']:7.1f} {100*r['frac_nominal_peak']:6.1f} "
+              f"{100*r['mfma_busy']:6.1f} {r['eff_clock_ghz_profiled']:5.2f} {r['hbm_gbs']:7.1f} {r['traffic_over_alg']:6.2f}")
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "run":
+        run("--time" in sys.argv)
+    else:
+        summary(*sys.argv[2:7])
