@@ -409,16 +409,20 @@ static const Config kConfigs[] = {
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
 static int prepare(int id) {
-  // raise the dynamic-LDS limit once per config (the reference re-does this
-  // inside every dispatch, :633/641/650/659)
-  static std::once_flag flags[kNumConfigs];
-  static hipError_t errs[kNumConfigs];
-  std::call_once(flags[id], [id] {
-    errs[id] = hipFuncSetAttribute((const void*)kConfigs[id].fn,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   kConfigs[id].info.lds_bytes);
+  // raise the dynamic-LDS limit once per (device, config) -- the reference
+  // re-does this inside every dispatch (:633/641/650/659).  Per device, so a
+  // process driving several GPUs (one host thread each) sets it on every one.
+  constexpr int kMaxDev = 64;
+  static std::once_flag flags[kMaxDev][kNumConfigs];
+  static hipError_t errs[kMaxDev][kNumConfigs];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return FA_ERR_HIP;
+  std::call_once(flags[dev][id], [dev, id] {
+    errs[dev][id] = hipFuncSetAttribute((const void*)kConfigs[id].fn,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        kConfigs[id].info.lds_bytes);
   });
-  return errs[id] == hipSuccess ? FA_OK : FA_ERR_HIP;
+  return errs[dev][id] == hipSuccess ? FA_OK : FA_ERR_HIP;
 }
 
 // causal rank-band width (query blocks of one head kept together on an XCD);
