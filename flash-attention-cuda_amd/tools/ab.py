@@ -67,6 +67,6 @@ for _ in range(a.rounds):
         res[c].append(flops / (st.elapsed_time(en) / a.iters / 1e3) / 1e12)
 names = {c.id: c.name for c in fa.configs()}
 for c in cids:
-    print(json.dumps({"config": names[c[1]], "lib": c[0] or "base", "seq": a.seq, "batch": a.batch, "heads": a.heads, "data": a.data, "causal": a.causal,
+    print(json.dumps({"config": names[c[1]], "lib": c[0] or "base", "env": a.env, "seq": a.seq, "batch": a.batch, "heads": a.heads, "data": a.data, "causal": a.causal,
                       "median_tflops": round(statistics.median(res[c]), 1),
                       "min_tflops": round(min(res[c]), 1), "max_tflops": round(max(res[c]), 1)}))
