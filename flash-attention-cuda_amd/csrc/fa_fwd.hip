@@ -425,16 +425,14 @@ static int prepare(int id) {
   return errs[dev][id] == hipSuccess ? FA_OK : FA_ERR_HIP;
 }
 
-// causal rank-band width (query blocks of one head kept together on an XCD);
-// FA_CAUSAL_BAND overrides the automatic choice for tuning (1 = plain
-// heaviest-first order)
-static int causal_band() {
-  static int band = [] {
-    const char* e = getenv("FA_CAUSAL_BAND");
-    return e ? atoi(e) : 0;  // 0 = automatic
-  }();
-  return band;
-}
+// causal rank-band width (query blocks of one head kept together on an XCD).
+// No run-time override in the product library: tuning builds set
+// -DFA_CAUSAL_BAND=<n> (1 = plain heaviest-first order), e.g.
+// `make variant-band16 VFLAGS=-DFA_CAUSAL_BAND=16`.
+#ifndef FA_CAUSAL_BAND
+#define FA_CAUSAL_BAND 0  // 0 = automatic
+#endif
+static_assert(FA_CAUSAL_BAND >= 0, "FA_CAUSAL_BAND: 0 (automatic) or a band width >= 1");
 
 // CUs of the current device (cached per device id)
 static int num_cus() {
@@ -481,7 +479,7 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   p.c = p.scale * 1.4426950408889634f;        // LOG2E, ref :239
   // few heads per XCD: plain heaviest-first balances better; many: keep the
   // query blocks of a head together for L2 reuse (profiles/r01_band_ab.txt)
-  p.band = causal_band() > 0 ? causal_band() : (bh <= 64 ? 1 : 16);
+  p.band = FA_CAUSAL_BAND > 0 ? FA_CAUSAL_BAND : (bh <= 64 ? 1 : 16);
   long long blocks = (long long)p.nqb * bh * num_splits;
   if (blocks > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
   if (cfg.kind == 2) {

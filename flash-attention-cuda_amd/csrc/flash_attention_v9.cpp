@@ -21,14 +21,13 @@ void flash_attention_v9_dispatch(const half* Q, const half* K, const half* V, ha
                                  float* splitk_buf_O, float* splitk_buf_ml, int batch_size,
                                  int num_heads, int seq_len, int head_dim, bool causal,
                                  hipStream_t stream) {
-  if (splitk_buf_O && splitk_buf_ml) {
-    // caller-provided split-K buffers (reference layout, :460-496): run the
-    // split-KV path with the library's split count (fa_splitkv_num_splits)
-    const int rc = fa_fwd_f16_splitkv(Q, K, V, Output, batch_size, num_heads, seq_len, head_dim,
-                                      causal ? 1 : 0, 0, splitk_buf_O, splitk_buf_ml, stream);
-    fa_check(rc, __FILE__, __LINE__);
-    return;
-  }
+  // The reference accepts the split-K buffers and never touches them (its
+  // dispatcher launches split_k = 1 only, :606-663).  Same here: a caller
+  // cannot learn a split count or buffer size through this signature, so
+  // writing into them could run past a buffer sized for the caller's own
+  // split count.  Split-KV is the explicit fa_fwd_f16_splitkv entry point.
+  (void)splitk_buf_O;
+  (void)splitk_buf_ml;
   const int rc = fa_fwd_f16(Q, K, V, Output, batch_size, num_heads, seq_len, head_dim,
                             causal ? 1 : 0, stream);
   fa_check(rc, __FILE__, __LINE__);

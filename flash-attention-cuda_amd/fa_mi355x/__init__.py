@@ -185,11 +185,12 @@ def kernel_attrs(config_id: int) -> dict:
     return {f: getattr(ka, f) for f, _ in _KernelAttrs._fields_}
 
 
-def _stream_handle(stream) -> Optional[int]:
+def _stream_handle(stream, device=None) -> Optional[int]:
+    """Raw hipStream_t of `stream` (None: torch's current stream on `device`)."""
     import torch
 
     if stream is None:
-        stream = torch.cuda.current_stream()
+        stream = torch.cuda.current_stream(device)
     if isinstance(stream, int):
         return stream
     return stream.cuda_stream
@@ -209,6 +210,9 @@ def _check_qkvo(q, k, v, out):
             raise FlashAttentionError(FA_ERR_BAD_SHAPE, f"{name} must be contiguous (BHSD)")
         if t.dim() != 4 or t.shape != q.shape:
             raise FlashAttentionError(FA_ERR_BAD_SHAPE, f"{name} must be [B,H,S,D] like q")
+        if t.device != q.device:
+            raise FlashAttentionError(FA_ERR_BAD_SHAPE,
+                                      f"{name} is on {t.device}, q on {q.device}: one device only")
 
 
 def flash_attention_fwd(q, k, v, causal: bool = False, out=None, config: Optional[int] = None,
@@ -228,15 +232,18 @@ def flash_attention_fwd(q, k, v, causal: bool = False, out=None, config: Optiona
     _check_qkvo(q, k, v, out)
     b, h, s, d = q.shape
     lib = load_library()
-    st = ctypes.c_void_p(_stream_handle(stream))
     args = (ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(k.data_ptr()),
             ctypes.c_void_p(v.data_ptr()), ctypes.c_void_p(out.data_ptr()), b, h, s, d,
             int(bool(causal)))
     bf16 = q.dtype == torch.bfloat16
-    if config is None:
-        _check((lib.fa_fwd_bf16 if bf16 else lib.fa_fwd_f16)(*args, st))
-    else:
-        _check((lib.fa_fwd_bf16_config if bf16 else lib.fa_fwd_f16_config)(*args, int(config), st))
+    # the C side launches on (and sizes for) the current device: make it q's
+    with torch.cuda.device(q.device):
+        st = ctypes.c_void_p(_stream_handle(stream, q.device))
+        if config is None:
+            _check((lib.fa_fwd_bf16 if bf16 else lib.fa_fwd_f16)(*args, st))
+        else:
+            _check((lib.fa_fwd_bf16_config if bf16 else lib.fa_fwd_f16_config)(*args, int(config),
+                                                                                st))
     return out
 
 
@@ -268,12 +275,17 @@ def flash_attention_fwd_splitkv(q, k, v, causal: bool = False, num_splits: int =
     need_ml = lib.fa_splitkv_ml_bytes(b, h, s, d, num_splits)
     if part_o.numel() * 4 < need_o or part_ml.numel() * 4 < need_ml:
         raise FlashAttentionError(FA_ERR_WORKSPACE, "split-KV buffers too small")
-    st = ctypes.c_void_p(_stream_handle(stream))
-    _check(lib.fa_fwd_f16_splitkv(
-        ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(k.data_ptr()),
-        ctypes.c_void_p(v.data_ptr()), ctypes.c_void_p(out.data_ptr()), b, h, s, d,
-        int(bool(causal)), int(num_splits), ctypes.c_void_p(part_o.data_ptr()),
-        ctypes.c_void_p(part_ml.data_ptr()), st))
+    for name, t in (("part_o", part_o), ("part_ml", part_ml)):
+        if t.device != q.device or t.dtype != torch.float32 or not t.is_contiguous():
+            raise FlashAttentionError(FA_ERR_WORKSPACE,
+                                      f"{name} must be contiguous float32 on {q.device}")
+    with torch.cuda.device(q.device):
+        st = ctypes.c_void_p(_stream_handle(stream, q.device))
+        _check(lib.fa_fwd_f16_splitkv(
+            ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(k.data_ptr()),
+            ctypes.c_void_p(v.data_ptr()), ctypes.c_void_p(out.data_ptr()), b, h, s, d,
+            int(bool(causal)), int(num_splits), ctypes.c_void_p(part_o.data_ptr()),
+            ctypes.c_void_p(part_ml.data_ptr()), st))
     return out
 
 
@@ -283,29 +295,35 @@ def flash_attention_v9_dispatch(Q, K, V, Output, splitk_buf_O, splitk_buf_ml, ba
     """Mirror of the reference host launch signature (flash_attention.cu:606-611).
 
     Q/K/V/Output are device tensors (or raw device pointers as ints) holding
-    BHSD fp16 data; splitk_buf_O/splitk_buf_ml may be None (ignored, as the
-    reference does) or reference-layout split-K buffers.  Raises
-    FlashAttentionError where the reference would exit(EXIT_FAILURE).
+    BHSD fp16 data on the current device.  splitk_buf_O/splitk_buf_ml are
+    accepted and ignored, as the reference's dispatcher ignores them (it only
+    launches split_k = 1; split-KV is :func:`flash_attention_fwd_splitkv`).
+    Raises FlashAttentionError where the reference would exit(EXIT_FAILURE).
     """
+    del splitk_buf_O, splitk_buf_ml
+
     def ptr(x):
-        if x is None:
-            return None
         return x if isinstance(x, int) else x.data_ptr()
 
     lib = load_library()
     st = ctypes.c_void_p(_stream_handle(stream) if stream not in (0, None) else None)
     q, k, v, o = (ctypes.c_void_p(ptr(x)) for x in (Q, K, V, Output))
-    if splitk_buf_O is not None and splitk_buf_ml is not None:
-        _check(lib.fa_fwd_f16_splitkv(q, k, v, o, batch_size, num_heads, seq_len, head_dim,
-                                      int(bool(causal)), 0,
-                                      ctypes.c_void_p(ptr(splitk_buf_O)),
-                                      ctypes.c_void_p(ptr(splitk_buf_ml)), st))
-    else:
-        _check(lib.fa_fwd_f16(q, k, v, o, batch_size, num_heads, seq_len, head_dim,
-                              int(bool(causal)), st))
+    _check(lib.fa_fwd_f16(q, k, v, o, batch_size, num_heads, seq_len, head_dim,
+                          int(bool(causal)), st))
 
 
 def attention_flops(batch: int, heads: int, seq_len: int, head_dim: int, causal: bool) -> float:
     """Reference FLOP convention: 4*B*H*S^2*D, halved when causal (:938-939)."""
     f = 4.0 * batch * heads * seq_len * seq_len * head_dim
     return f / 2 if causal else f
+
+
+def kernel_symbol(config_name: str) -> str:
+    """Substring of the kernel symbol rocprofv3 reports for a tile config."""
+    if "persistent" in config_name:
+        return "fa_fwd_f16_persistent_kernel"
+    if "kvpair" in config_name or "kvquad" in config_name:
+        return "fa_fwd_f16_kvpair_kernel"
+    if "splitkv" in config_name:
+        return "fa_fwd_f16_splitkv_kernel"
+    return "fa_fwd_f16_kernel"

@@ -52,6 +52,11 @@ def main():
                   "bench.py --steps 3 --warmup 1 --no-sweep --no-cpu-baseline; mean over "
                   "dispatches 2..N; FETCH x1024 x2 (gfx950 half-count), WRITE x1024",
     }
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+    import bench
+
+    d["source_digest"] = bench.source_digest()
+    d["git_head"] = os.environ.get("GIT_HEAD")
     with open(out, "w") as f:
         json.dump(d, f, indent=1)
     print(json.dumps(d))

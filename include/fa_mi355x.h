@@ -31,7 +31,7 @@ extern "C" {
 typedef enum {
   FA_OK = 0,
   FA_ERR_NULL_POINTER = 1,        /* q/k/v/o NULL with a non-empty problem */
-  FA_ERR_UNSUPPORTED_HEAD_DIM = 2,/* only head_dim == 128 (ref :613 HD=128) */
+  FA_ERR_UNSUPPORTED_HEAD_DIM = 2,/* head_dim not 128 (ref :613 HD=128) or 64 */
   FA_ERR_BAD_SHAPE = 3,           /* negative sizes or int overflow of B*H */
   FA_ERR_LAUNCH = 4,              /* hipGetLastError() after the launch */
   FA_ERR_BAD_CONFIG = 5,          /* config id out of range / wrong causal */

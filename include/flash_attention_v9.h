@@ -12,11 +12,10 @@
  * 1/sqrt(head_dim), asynchronous on `stream`, returns void, and on any error
  * prints "HIP error at <file>:<line>: <msg>" and exit(EXIT_FAILURE) exactly
  * as CUDA_CHECK(cudaGetLastError()) does (:22-30, :662).
- * splitk_buf_O / splitk_buf_ml: the reference accepts and ignores them
- * (callers pass nullptr, :777).  Here, when BOTH are non-null they are used
- * as the split-KV buffers in the reference's layout (fa_fwd_f16_splitkv, with
- * fa_splitkv_num_splits() splits; sizes fa_splitkv_o_bytes/_ml_bytes);
- * otherwise they are ignored as in the reference.
+ * splitk_buf_O / splitk_buf_ml: accepted and ignored, as in the reference
+ * (its dispatcher never launches the split-K path; callers pass nullptr,
+ * :777).  Split-KV is the explicit C entry fa_fwd_f16_splitkv (fa_mi355x.h),
+ * which takes the split count and the buffers explicitly.
  */
 #ifndef FLASH_ATTENTION_V9_H
 #define FLASH_ATTENTION_V9_H

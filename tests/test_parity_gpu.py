@@ -145,3 +145,22 @@ def test_error_codes():
     with pytest.raises(fa.FlashAttentionError) as e:
         fa.flash_attention_v9_dispatch(q, q, q, q, None, None, 1, 1, 64, 96, False)
     assert e.value.status == fa.FA_ERR_UNSUPPORTED_HEAD_DIM
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                    reason="needs two GPUs")
+def test_non_current_device():
+    """Tensors on cuda:1 while cuda:0 is current: the launch goes to cuda:1
+    (the C side sizes and launches on the current device, so the binding
+    switches to q's device); tensors split over devices are rejected."""
+    fa = _fa()
+    q, k, v, ref = _case(1, 4, 256, True)
+    torch.cuda.set_device(0)
+    d1 = torch.device("cuda", 1)
+    dq, dk, dv = (torch.from_numpy(a.view(np.int16)).view(torch.float16).to(d1) for a in (q, k, v))
+    o = fa.flash_attention_fwd(dq, dk, dv, causal=True)
+    torch.cuda.synchronize(d1)
+    assert o.device == d1
+    assert oracle.max_abs_diff(_to_host_bits(o), ref) <= TOL
+    with pytest.raises(fa.FlashAttentionError):
+        fa.flash_attention_fwd(dq, dk.to("cuda:0"), dv, causal=True)

@@ -99,3 +99,46 @@ def test_persistent_nc_tail_split(kind):
         ref = oracle.attention(*(_bits(x[sl]) for x in (q, k, v)), False)
         d = oracle.max_abs_diff(_bits(out[sl]), ref)
         assert d <= TOL, f"head {flat}: max_diff={d}"
+
+
+def _torch_ref(q, k, v, causal):
+    """fp32 reference of the same op (for bf16 / head_dim 64, which the
+    reference's fp16 d128 oracle does not cover)."""
+    qf, kf, vf = q.float(), k.float(), v.float()
+    sc = qf @ kf.transpose(-1, -2) / (q.shape[-1] ** 0.5)
+    if causal:
+        s = q.shape[2]
+        sc = sc + torch.full((s, s), float("-inf"), device=q.device).triu(1)
+    return (torch.softmax(sc, dim=-1) @ vf).to(q.dtype)
+
+
+def _cfg(dtype, head_dim, causal):
+    fa = _fa()
+    for c in fa.configs():
+        if (c.dtype == dtype and c.head_dim == head_dim and c.causal == causal
+                and "pingpong_persistent" in c.name and "dma" not in c.name):
+            return c.id
+    raise AssertionError((dtype, head_dim, causal))
+
+
+# Ragged tail split: S=1900 gives 8 query blocks of 256 rows, the last one
+# ragged; B=1 H=48 puts 48 items on each XCD's 32 CUs, so the last 16 (heads
+# 32..47) run as KV-pair halves -- half 14 partly and half 15 entirely past S.
+@pytest.mark.parametrize("dtype,head_dim", [("float16", 128), ("bfloat16", 128),
+                                            ("float16", 64), ("bfloat16", 64)])
+def test_persistent_nc_tail_split_ragged(dtype, head_dim):
+    fa = _fa()
+    b, h, s = 1, 48, 1900
+    tdt = torch.float16 if dtype == "float16" else torch.bfloat16
+    q, k, v = (_rand((b, h, s, head_dim), 400 + i).to(tdt) for i in range(3))
+    out = fa.flash_attention_fwd(q, k, v, causal=False, config=_cfg(dtype, head_dim, False))
+    torch.cuda.synchronize()
+    ref = _torch_ref(q, k, v, False)
+    tol = TOL if dtype == "float16" else 5e-3  # bf16: 8 significant bits (tests/test_bf16_gpu.py)
+    err = (out.float() - ref.float()).abs()
+    assert err.max().item() <= tol, f"max err {err.max().item()}"
+    if dtype == "float16" and head_dim == 128:
+        for flat in (32, 47):  # tail items, against the oracle too
+            sl = (slice(0, 1), slice(flat, flat + 1))
+            r = oracle.attention(*(_bits(x[sl]) for x in (q, k, v)), False)
+            assert oracle.max_abs_diff(_bits(out[sl]), r) <= TOL
