@@ -19,6 +19,7 @@ step bench &&
 timeout -k 10 900 python bench.py > $OUT/bench.json 2> $OUT/bench.err &&
 step rocprof-kernel-trace &&
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_kt -o kt --output-format csv -- python bench.py --no-sweep --no-cpu-baseline --no-pmc > $OUT/bench_under_kt.json 2> $OUT/prof_kt.log &&
+python flash-attention-cuda_amd/tools/kt_timed_avg.py $OUT/prof_kt/kt_kernel_trace.csv $OUT/bench_under_kt.json > $OUT/kt_timed_avg.json &&
 step harness &&
 FA_COOLDOWN_S=2 timeout -k 10 600 tests/harness/build/flash_attention > $OUT/harness.log 2>&1
 rc=$?
