@@ -71,12 +71,12 @@ __device__ __forceinline__ void map_block(int id, int nblk, int nqb, int bh_coun
 // BF16: Q/K/V/O and the MFMA operands are bf16 (16x16x32 policy only)
 // HDIM: head_dim (64 runs on the 16x16x32 policy only)
 template <int WAVES, int BN, bool CAUSAL, bool SPLIT, bool USE_M16, int SCHED, bool BF16 = false,
-          int HDIM = 128>
+          int HDIM = 128, int QB = 2>
 __device__ __forceinline__ void run_tile_loop(const FwdParams& p, int bh, int qb, int split,
                                               char* smem) {
   static_assert(USE_M16 || (!BF16 && HDIM == 128), "bf16 / head_dim 64 run on the 16x16x32 policy");
   using Pol = typename std::conditional<
-      USE_M16, M16<BN, typename std::conditional<BF16, __bf16, f16>::type, HDIM>, M32<BN>>::type;
+      USE_M16, M16<BN, typename std::conditional<BF16, __bf16, f16>::type, HDIM, QB>, M32<BN>>::type;
   if constexpr (SCHED == 1 || SCHED == 2 || SCHED == 3) {
     static_assert(WAVES == 8, "ping-pong needs two groups of four waves");
     attention_pingpong<Pol, CAUSAL, SPLIT, SCHED != 2, SCHED == 3>(p, bh, qb, split, smem);
@@ -85,9 +85,11 @@ __device__ __forceinline__ void run_tile_loop(const FwdParams& p, int bh, int qb
   }
 }
 
+// QB = 4: 64 query rows per wave, one wave per SIMD (the whole 512-entry
+// register file per wave)
 template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED, bool BF16 = false,
-          int HDIM = 128>
-__global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_kernel(FwdParams p) {
+          int HDIM = 128, int QB = 2>
+__global__ __launch_bounds__(WAVES * 64, QB == 4 ? 1 : 2) void fa_fwd_f16_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 #ifdef FA_STAMPS
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
@@ -95,7 +97,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_kernel(FwdParams p) 
 #endif
   int qb, bh;
   map_block(blockIdx.x, gridDim.x, p.nqb, p.bh, p.band, CAUSAL, qb, bh);
-  run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED, BF16, HDIM>(p, bh, qb, 0, smem);
+  run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED, BF16, HDIM, QB>(p, bh, qb, 0, smem);
 #ifdef FA_STAMPS
   if (threadIdx.x == 0 && blockIdx.x < FA_MAX_TIMELINE) {
     unsigned hw, xcc;
@@ -177,8 +179,9 @@ struct XcdItems {
 };
 
 template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED, bool BF16 = false,
-          int HDIM = 128>
-__global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(FwdParams p) {
+          int HDIM = 128, int QB = 2>
+__global__ __launch_bounds__(WAVES * 64, QB == 4 ? 1 : 2) void fa_fwd_f16_persistent_kernel(
+    FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int x = blockIdx.x & 7, lcu = blockIdx.x >> 3, C = gridDim.x >> 3;
   const XcdItems<CAUSAL> items(p, x);
@@ -204,7 +207,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(Fw
       const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
       const unsigned long long c_start = __builtin_amdgcn_s_memtime();
 #endif
-      run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED, BF16, HDIM>(p, bh, qb, 0, smem);
+      run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED, BF16, HDIM, QB>(p, bh, qb, 0, smem);
 #ifdef FA_STAMPS
       const int rec = bh * p.nqb + qb;
       if (threadIdx.x == 0 && rec < FA_MAX_TIMELINE) {
@@ -315,7 +318,7 @@ struct Config {
   kernel_fn fn;
 };
 
-template <int W, int BN_, int C, int SPL, int M, int SCHED, int DT, int HDIM>
+template <int W, int BN_, int C, int SPL, int M, int SCHED, int DT, int HDIM, int QB = 2>
 constexpr kernel_fn pick_kernel() {
   if constexpr (SPL == 3)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
@@ -325,9 +328,9 @@ constexpr kernel_fn pick_kernel() {
   else if constexpr (SPL == 1)
     return fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
   else if constexpr (SPL == 2)
-    return fa_fwd_f16_persistent_kernel<W, BN_, (C != 0), (M == 16), SCHED, DT == 1, HDIM>;
+    return fa_fwd_f16_persistent_kernel<W, BN_, (C != 0), (M == 16), SCHED, DT == 1, HDIM, QB>;
   else
-    return fa_fwd_f16_kernel<W, BN_, (C != 0), (M == 16), SCHED, DT == 1, HDIM>;
+    return fa_fwd_f16_kernel<W, BN_, (C != 0), (M == 16), SCHED, DT == 1, HDIM, QB>;
 }
 
 // KIND: 0 = one workgroup per (head, query block), 1 = split-KV, 2 = persistent
@@ -351,6 +354,12 @@ constexpr kernel_fn pick_kernel() {
 #define FA_CFG_KVQUAD(ID, C, DT, HDIM, NAME)                                           \
   {{ID, 64, 64, 8, C, 0, kKvquadLdsBytes, NAME, DT, HDIM}, 16, 1, 4,                    \
    pick_kernel<8, 64, C, 4, 16, 1, DT, HDIM>()}
+
+// 4 waves x 64 query rows (one wave per SIMD, 512 registers each), one
+// barrier per tile: half the LDS bytes per FLOP of the 32-row waves
+#define FA_CFG_W4X64(ID, C, KIND, SCHED, NAME)                                  \
+  {{ID, 256, 64, 4, C, 0, 4 * 64 * ROW_BYTES, NAME, 0, 128}, 16, SCHED, KIND,    \
+   pick_kernel<4, 64, C, KIND, 16, SCHED, 0, 128, 4>()}
 
 static const Config kConfigs[] = {
     FA_CFG(0, 4, 64, 0, 0, 32, 0, "bm128_bn64_w4_m32_noncausal"),
@@ -405,6 +414,11 @@ static const Config kConfigs[] = {
     FA_CFG_KVQUAD(43, 1, 0, 64, "d64_bm64_bn64_w8_m16_kvquad_causal"),
     FA_CFG_KVQUAD(44, 0, 1, 64, "bf16_d64_bm64_bn64_w8_m16_kvquad_noncausal"),
     FA_CFG_KVQUAD(45, 1, 1, 64, "bf16_d64_bm64_bn64_w8_m16_kvquad_causal"),
+    // 64 query rows per wave (QB = 4), per-item and persistent
+    FA_CFG_W4X64(46, 0, 0, 0, "bm256_bn64_w4x64_m16_noncausal"),
+    FA_CFG_W4X64(47, 1, 0, 0, "bm256_bn64_w4x64_m16_causal"),
+    FA_CFG_W4X64(48, 0, 2, 0, "bm256_bn64_w4x64_m16_persistent_noncausal"),
+    FA_CFG_W4X64(49, 1, 2, 0, "bm256_bn64_w4x64_m16_persistent_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 

@@ -197,6 +197,7 @@ struct M32 {
   static constexpr int HDIM = 128;  // head_dim 128 only
   static constexpr int RPW = 4;     // tile rows one wave stages per pass
   static constexpr int NSB = BN / 32;  // 32-key S^T blocks per tile
+  static constexpr int RW = 32;        // query rows per wave
   int lane, r, h;
   int kaddr0, kaddr1, vaddr0, vaddr1;
   f16x8 qf[8];
@@ -432,7 +433,7 @@ struct Elem {
   }
 };
 
-template <int BN_, class T = f16, int HDIM_ = 128>
+template <int BN_, class T = f16, int HDIM_ = 128, int QB_ = 2>
 struct M16 {
   static_assert(HDIM_ == 64 || HDIM_ == 128, "head_dim 64 or 128");
   static constexpr int BN = BN_;
@@ -446,17 +447,19 @@ struct M16 {
   // the head_dim-128 one.
   static constexpr int NKB = BN / 16;  // 16-key blocks per tile
   static constexpr int NU = BN / 32;   // 32-key PV steps per tile
+  static constexpr int QB = QB_;       // 16-row query blocks per wave (2: 32 rows, 4: 64 rows)
+  static constexpr int RW = 16 * QB;   // query rows per wave
   typedef typename Elem<T>::x8 tx8;
   typedef typename Elem<T>::x4 tx4;
   int lane, r16, g, sg;
   int kaddr[4], vaddr[2];
-  tx8 qf[2][NTQ];
-  f32x4 acc[2][NE];
-  f32x4 s[2][NKB];
-  tx8 pf[2][NU];
-  f32x4 negm[2];     // C operand of the QK^T chains: -m_ref broadcast
-  float m_ref[2];    // reference max, log2 units (x = s*c - m_ref)
-  f32x4 lacc[2];     // running row sums l (ones . P on the matrix pipe, in the PV chain)
+  tx8 qf[QB][NTQ];
+  f32x4 acc[QB][NE];
+  f32x4 s[QB][NKB];
+  tx8 pf[QB][NU];
+  f32x4 negm[QB];     // C operand of the QK^T chains: -m_ref broadcast
+  float m_ref[QB];    // reference max, log2 units (x = s*c - m_ref)
+  f32x4 lacc[QB];     // running row sums l (ones . P on the matrix pipe, in the PV chain)
   bool have_ref;     // wave-uniform: a tile has set m_ref
   float c;
 
@@ -475,7 +478,7 @@ struct M16 {
       vaddr[ep] = 2048 * (sg >> 1) + 64 * (4 * (sg & 1) + qq) + 16 * ((2 * ep + (pp >> 1)) ^ sg) +
                   8 * (pp & 1);
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < QB; ++b) {
 #pragma unroll
       for (int e = 0; e < NE; ++e) acc[b][e] = f32x4{};
       negm[b] = f32x4{};
@@ -487,7 +490,7 @@ struct M16 {
   // Q: qf[b][t] = c * Q[qw + 16b + r16][32t + 8g .. +7]   (rounded to fp16)
   __device__ __forceinline__ void issue_q(__amdgpu_buffer_rsrc_t rq, int qw) {
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < QB; ++b)
 #pragma unroll
       for (int t = 0; t < NTQ; ++t)
         qf[b][t] = __builtin_bit_cast(
@@ -495,7 +498,7 @@ struct M16 {
   }
   __device__ __forceinline__ void scale_q() {
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < QB; ++b)
 #pragma unroll
       for (int t = 0; t < NTQ; ++t)
 #pragma unroll
@@ -507,9 +510,68 @@ struct M16 {
   // every tile load issued since (a full memory latency per item)
   __device__ __forceinline__ void pin_q() {
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < QB; ++b)
 #pragma unroll
-      for (int t = 0; t < NTQ; ++t) asm volatile("" : "+v"(qf[b][t]));
+      for (int t = 0; t < NTQ; ++t) {
+        if constexpr (kAsm)
+          asm volatile("" : "+a"(qf[b][t]));
+        else
+          asm volatile("" : "+v"(qf[b][t]));
+      }
+  }
+  // ---- QB = 4: 64 query rows per wave, one wave per SIMD (512 registers) ----
+  // hipcc left to itself routes the S tile through AGPRs (a v_accvgpr copy
+  // per element and pass) and spills (tools/experiments/w4_spill_probe.sh).
+  // Here every MFMA is an inline-asm statement with pinned register classes:
+  // O, l and Q in AGPRs ("a"), S and P in VGPRs ("v").  hipcc pads nothing
+  // inside asm, so the hazards are padded in the statements:
+  //  * "s_nop 2" ahead of each MFMA: a VALU-written operand (P, negm, an
+  //    accvgpr-written O) needs its wait states; between back-to-back MFMAs
+  //    the nop issues in the matrix pipe's shadow;
+  //  * mfma_pad_*: 18 wait states between the last MFMA writing S (or O)
+  //    and the first VALU reading it, ordered through "+v"/"+a" operands.
+  static constexpr bool kAsm = QB == 4;
+  static_assert(!kAsm || std::is_same<T, f16>::value, "asm MFMA path: fp16");
+  __device__ __forceinline__ void mfma_pad_s() {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 1"
+                 : "+v"(s[0][0]), "+v"(s[0][1]), "+v"(s[0][2]), "+v"(s[0][3]), "+v"(s[1][0]),
+                   "+v"(s[1][1]), "+v"(s[1][2]), "+v"(s[1][3]), "+v"(s[2][0]), "+v"(s[2][1]),
+                   "+v"(s[2][2]), "+v"(s[2][3]), "+v"(s[3][0]), "+v"(s[3][1]), "+v"(s[3][2]),
+                   "+v"(s[3][3]));
+  }
+  // S block = K . Q^T step: first of a chain (C = -m_ref) or accumulate
+  __device__ __forceinline__ void mma_s0(f32x4& d, tx8 kf, const tx8& q, f32x4 c) {
+    if constexpr (kAsm)
+      asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %3" : "=&v"(d) : "v"(kf), "a"(q), "v"(c));
+    else
+      d = Elem<T>::mfma(kf, q, c);
+  }
+  __device__ __forceinline__ void mma_s(f32x4& d, tx8 kf, const tx8& q) {
+    if constexpr (kAsm)
+      asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(d) : "v"(kf), "a"(q));
+    else
+      d = Elem<T>::mfma(kf, q, d);
+  }
+  // O (or l) += V^T-fragment . P
+  __device__ __forceinline__ void mma_o(f32x4& d, tx8 vf, const tx8& p) {
+    if constexpr (kAsm)
+      asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(d) : "v"(vf), "v"(p));
+    else
+      d = Elem<T>::mfma(vf, p, d);
+  }
+  __device__ __forceinline__ void mfma_pad_o() {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 1"
+                 : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[0][2]), "+a"(acc[0][3]),
+                   "+a"(acc[0][4]), "+a"(acc[0][5]), "+a"(acc[0][6]), "+a"(acc[0][7]),
+                   "+a"(acc[1][0]), "+a"(acc[1][1]), "+a"(acc[1][2]), "+a"(acc[1][3]),
+                   "+a"(acc[1][4]), "+a"(acc[1][5]), "+a"(acc[1][6]), "+a"(acc[1][7]),
+                   "+a"(lacc[0]), "+a"(lacc[1]));
+    asm volatile(""
+                 : "+a"(acc[2][0]), "+a"(acc[2][1]), "+a"(acc[2][2]), "+a"(acc[2][3]),
+                   "+a"(acc[2][4]), "+a"(acc[2][5]), "+a"(acc[2][6]), "+a"(acc[2][7]),
+                   "+a"(acc[3][0]), "+a"(acc[3][1]), "+a"(acc[3][2]), "+a"(acc[3][3]),
+                   "+a"(acc[3][4]), "+a"(acc[3][5]), "+a"(acc[3][6]), "+a"(acc[3][7]),
+                   "+a"(lacc[2]), "+a"(lacc[3]));
   }
   __device__ __forceinline__ void load_q(__amdgpu_buffer_rsrc_t rq, int qw) {
     issue_q(rq, qw);
@@ -536,6 +598,27 @@ struct M16 {
   static __device__ __forceinline__ int v_src(int o) { return lds_off_src(o); }
 
   __device__ __forceinline__ void qk(const char* kb) {
+    if constexpr (kAsm) {
+#pragma unroll
+      for (int t = 0; t < NTQ; ++t)
+#pragma unroll
+        for (int cb = 0; cb < NKB; ++cb) {
+          const tx8 kf = *reinterpret_cast<const tx8*>(kb + kaddr[t] + 4096 * cb);
+#pragma unroll
+          for (int b = 0; b < QB; ++b) {
+            if (t == 0)
+              asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %3"
+                  : "=&v"(s[b][cb])
+                  : "v"(kf), "a"(qf[b][t]), "v"(negm[b]));
+            else
+              asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0"
+                  : "+v"(s[b][cb])
+                  : "v"(kf), "a"(qf[b][t]));
+          }
+        }
+      mfma_pad_s();
+      return;
+    }
 #pragma unroll
     for (int t = 0; t < NTQ; ++t)
 #pragma unroll
@@ -546,14 +629,14 @@ struct M16 {
         const tx8 kf = *reinterpret_cast<const tx8*>(kb + kaddr[t] + 4096 * cb);
 #endif
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < QB; ++b)
           s[b][cb] = Elem<T>::mfma(kf, qf[b][t], t == 0 ? negm[b] : s[b][cb]);
       }
   }
   // P = exp2(x) -> fp16, already in the B-operand layout of the PV product
   __device__ __forceinline__ void exp_p() {
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < QB; ++b)
 #pragma unroll
       for (int cb = 0; cb < NKB; ++cb)
 #pragma unroll
@@ -570,7 +653,7 @@ struct M16 {
   __device__ __forceinline__ void softmax(int kv0, int kv_hi, int qw, float /*c*/, bool need_mask) {
     if (need_mask) {
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
+      for (int b = 0; b < QB; ++b) {
         const int qrow = qw + 16 * b + r16;
 #pragma unroll
         for (int cb = 0; cb < NKB; ++cb)
@@ -584,10 +667,10 @@ struct M16 {
     }
     // row max relative to m_ref; shift m_ref (and rescale O, l) only when it
     // grew by more than RESCALE_LOG2 -- P then stays <= 2^RESCALE_LOG2
-    float mx[2];
+    float mx[QB];
     bool grow = !have_ref;
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < QB; ++b) {
       float m = s[b][0][0];
 #pragma unroll
       for (int cb = 0; cb < NKB; ++cb)
@@ -606,15 +689,18 @@ struct M16 {
     if (__any(grow)) {
 #ifndef FA_ROWMAX_ALWAYS
 #pragma unroll
-      for (int b = 0; b < 2; ++b) mx[b] = max_xor32(max_xor16(mx[b]));
+      for (int b = 0; b < QB; ++b) mx[b] = max_xor32(max_xor16(mx[b]));
 #endif
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
+      for (int b = 0; b < QB; ++b) {
         // first tile: centre on the max; later: only ever move m_ref up.
         // A row with every key masked (mx = -inf) keeps m_ref.
         float sh = have_ref ? fmaxf(mx[b], 0.f) : mx[b];
         sh = sh == ninf() ? 0.f : sh;
         if (have_ref) {
+          if constexpr (kAsm) {
+            if (b == 0) mfma_pad_o();
+          }
           const float alpha = __builtin_amdgcn_exp2f(-sh);
 #pragma unroll
           for (int e = 0; e < NE; ++e) acc[b][e] *= alpha;
@@ -629,8 +715,208 @@ struct M16 {
     }
     exp_p();
   }
+  // ---- split softmax for the one-wave-per-SIMD pipeline (attention_w4) ----
+  // softmax(j) runs beside PV(j-1) and is cut where its rare, wave-uniform
+  // rescale decision sits:
+  //   sm_max   : mask, per-lane partial row maxima, "some row grew" flag
+  //   sm_shift : (rare) move m_ref, shift S, remember alpha for O and l
+  //   sm_exp   : P = exp2(S) in place (fp32, still in the S registers)
+  //   sm_alpha : (rare) O, l *= alpha -- after PV(j-1) has accumulated,
+  //              since that tile's P was relative to the old m_ref
+  //   cvt_p    : S -> fp16 P (the PV B operand), beside QK^T(j+1), whose
+  //              MFMAs then overwrite the S registers
+  float alpha[QB];
+  template <bool CAUSAL>
+  __device__ __forceinline__ bool sm_max(int kv0, int kv_hi, int qw, bool need_mask) {
+    if (need_mask) {
+#pragma unroll
+      for (int b = 0; b < QB; ++b) {
+        const int qrow = qw + 16 * b + r16;
+#pragma unroll
+        for (int cb = 0; cb < NKB; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int kv = kv0 + 16 * cb + 4 * sg + i;
+            const bool ok = kv < kv_hi && (!CAUSAL || kv <= qrow);
+            s[b][cb][i] = ok ? s[b][cb][i] : ninf();
+          }
+      }
+    }
+    bool grow = !have_ref;
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      float m = s[b][0][0];
+#pragma unroll
+      for (int cb = 0; cb < NKB; ++cb)
+#pragma unroll
+        for (int i = (cb == 0 ? 1 : 0); i < 4; ++i) m = fmaxf(m, s[b][cb][i]);
+      mx_[b] = m;
+      grow |= m > RESCALE_LOG2;
+    }
+    return __any(grow);
+  }
+  float mx_[QB];
+  // returns true when O and l must be rescaled (sm_alpha) after PV(j-1)
+  __device__ __forceinline__ bool sm_shift() {
+    const bool had = have_ref;
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      const float mxb = max_xor32(max_xor16(mx_[b]));
+      // first tile: centre on the max; later: only ever move m_ref up.
+      // A row with every key masked (mx = -inf) keeps m_ref.
+      float sh = had ? fmaxf(mxb, 0.f) : mxb;
+      sh = sh == ninf() ? 0.f : sh;
+      alpha[b] = __builtin_amdgcn_exp2f(-sh);
+#pragma unroll
+      for (int cb = 0; cb < NKB; ++cb) s[b][cb] -= sh;
+      m_ref[b] += sh;
+      negm[b] = f32x4{-m_ref[b], -m_ref[b], -m_ref[b], -m_ref[b]};
+    }
+    have_ref = true;
+    return had;
+  }
+  __device__ __forceinline__ void sm_exp() {
+#pragma unroll
+    for (int b = 0; b < QB; ++b)
+#pragma unroll
+      for (int cb = 0; cb < NKB; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[b][cb][i] = __builtin_amdgcn_exp2f(s[b][cb][i]);
+  }
+  // x *= a for an accumulator tuple; asm path: through 4 VGPRs and back into
+  // the same AGPR class, one tuple at a time
+  __device__ __forceinline__ void scale_acc(f32x4& x, float a) {
+    if constexpr (kAsm) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float t;
+        asm volatile(
+            "v_accvgpr_read_b32 %1, %0\n\t"
+            "v_mul_f32_e32 %1, %1, %2\n\t"
+            "v_accvgpr_write_b32 %0, %1"
+            : "+a"(x[i]), "=&v"(t)
+            : "v"(a));
+      }
+    } else {
+      x *= a;
+    }
+  }
+  // one 4-register accumulator tuple at a time (sched_barrier): scheduled
+  // freely, hipcc reads all 144 AGPRs ahead of the multiplies and the
+  // temporaries spill the pipelined loop
+  __device__ __forceinline__ void sm_alpha() {
+    if constexpr (kAsm) mfma_pad_o();
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+#pragma unroll
+      for (int e = 0; e < NE; ++e) scale_acc(acc[b][e], alpha[b]);
+      scale_acc(lacc[b], alpha[b]);
+    }
+  }
+  // W4 pipeline with P double-buffered (P(j) is written beside the PV(j-1)
+  // MFMAs that read P(j-1)): buffer PB of {pf, pf2}
+  tx8 pf2[QB][NU];
+  template <int PB>
+  __device__ __forceinline__ tx8 (&pbuf())[QB][NU] {
+    if constexpr (PB == 0) return pf; else return pf2;
+  }
+  template <int PB>
+  __device__ __forceinline__ void exp_cvt() {
+    tx8 (&P)[QB][NU] = pbuf<PB>();
+#pragma unroll
+    for (int b = 0; b < QB; ++b)
+#pragma unroll
+      for (int cb = 0; cb < NKB; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) P[b][cb >> 1][4 * (cb & 1) + i] = (T)__builtin_amdgcn_exp2f(s[b][cb][i]);
+  }
+  template <int PB>
+  __device__ __forceinline__ void pv_buf(const char* vb) {
+    tx8 (&P)[QB][NU] = pbuf<PB>();
+    const tx8 ones = {(T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f};
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const int base = 8192 * u + 512 * (e >> 1) + vaddr[e & 1];
+        const tx4 lo = __builtin_bit_cast(tx4, lds_read_tr(vb, base));
+        const tx4 hi = __builtin_bit_cast(tx4, lds_read_tr(vb, base + 4096));
+        const tx8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int b = 0; b < QB; ++b) mma_o(acc[b][e], vf, P[b][u]);
+      }
+#pragma unroll
+      for (int b = 0; b < QB; ++b) mma_o(lacc[b], ones, P[b][u]);
+    }
+  }
+  // chain-major QK^T: each S block's 4-deep chain back to back (a dependent
+  // 16x16x32 chain issues at full rate), so S blocks complete one by one and
+  // their row maxima can start beside the remaining MFMAs
+  __device__ __forceinline__ void qk_cm(const char* kb) {
+#pragma unroll
+    for (int cb = 0; cb < NKB; ++cb) {
+      tx8 kf[NTQ];
+#pragma unroll
+      for (int t = 0; t < NTQ; ++t) kf[t] = *reinterpret_cast<const tx8*>(kb + kaddr[t] + 4096 * cb);
+#pragma unroll
+      for (int b = 0; b < QB; ++b)
+#pragma unroll
+        for (int t = 0; t < NTQ; ++t) {
+          if (t == 0) mma_s0(s[b][cb], kf[t], qf[b][t], negm[b]);
+          else mma_s(s[b][cb], kf[t], qf[b][t]);
+        }
+    }
+    if constexpr (kAsm) mfma_pad_s();
+  }
+  __device__ __forceinline__ void cvt_p() {
+#pragma unroll
+    for (int b = 0; b < QB; ++b)
+#pragma unroll
+      for (int cb = 0; cb < NKB; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pf[b][cb >> 1][4 * (cb & 1) + i] = (T)s[b][cb][i];
+  }
+
+  // one 32-key half (u) of the PV product and its row-sum MFMAs
+  __device__ __forceinline__ void pv_half(const char* vb, int u) {
+    const tx8 ones = {(T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f};
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int base = 8192 * u + 512 * (e >> 1) + vaddr[e & 1];
+      const tx4 lo = __builtin_bit_cast(tx4, lds_read_tr(vb, base));
+      const tx4 hi = __builtin_bit_cast(tx4, lds_read_tr(vb, base + 4096));
+      const tx8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+      for (int b = 0; b < QB; ++b) mma_o(acc[b][e], vf, pf[b][u]);
+    }
+#pragma unroll
+    for (int b = 0; b < QB; ++b) mma_o(lacc[b], ones, pf[b][u]);
+  }
   __device__ __forceinline__ void pv(const char* vb) {
     const tx8 ones = {(T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f};
+    if constexpr (kAsm) {
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const int base = 8192 * u + 512 * (e >> 1) + vaddr[e & 1];
+          const tx4 lo = __builtin_bit_cast(tx4, lds_read_tr(vb, base));
+          const tx4 hi = __builtin_bit_cast(tx4, lds_read_tr(vb, base + 4096));
+          const tx8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+          for (int b = 0; b < QB; ++b)
+            asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0"
+                : "+a"(acc[b][e])
+                : "v"(vf), "v"(pf[b][u]));
+        }
+#pragma unroll
+        for (int b = 0; b < QB; ++b)
+          asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0"
+              : "+a"(lacc[b])
+              : "v"(ones), "v"(pf[b][u]));
+      }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
 #pragma unroll
@@ -644,13 +930,13 @@ struct M16 {
         const tx8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 #endif
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < QB; ++b)
           acc[b][e] = Elem<T>::mfma(vf, pf[b][u], acc[b][e]);
       }
       // row sums of the same fp16 P: every register of lacc[b] = l for q = lane&15
 #ifndef FA_ROWSUM_VALU
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < QB; ++b)
         lacc[b] = Elem<T>::mfma(ones, pf[b][u], lacc[b]);
 #endif
     }
@@ -721,8 +1007,9 @@ struct M16 {
   // (dwordx4 instead of dwordx2) at the same bytes; the store tail is
   // issue-bound (guide T21).
   __device__ __forceinline__ void store_o(__amdgpu_buffer_rsrc_t ro, int qw) {
+    if constexpr (kAsm) mfma_pad_o();
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < QB; ++b) {
       const float lt = row_sum(b);  // already the full row sum (MFMA over all keys)
       const float inv = lt > 0.f ? 1.0f / lt : 0.f;
       const int rowb = (qw + 16 * b + r16) * ROW;
@@ -762,19 +1049,21 @@ struct M16 {
   // Region per wave: 2*NE f32x4 of O, then one f32x4 {m_0, l_0, m_1, l_1}.
   static constexpr int MERGE_BYTES = (2 * NE + 1) * 64 * 16;
   __device__ __forceinline__ void put_partial(char* region) const {
+    static_assert(QB == 2, "KV-pair merge layout: two query blocks per wave");
     f32x4* d = reinterpret_cast<f32x4*>(region);
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < QB; ++b)
 #pragma unroll
       for (int e = 0; e < NE; ++e) d[(b * NE + e) * 64 + lane] = acc[b][e];
     d[2 * NE * 64 + lane] = f32x4{m_ref[0], row_sum(0), m_ref[1], row_sum(1)};
   }
   // O = O_a 2^(m_a-M) + O_b 2^(m_b-M), l likewise, M = max over partials that saw a key
   __device__ __forceinline__ void merge_partial(const char* region) {
+    static_assert(QB == 2, "KV-pair merge layout: two query blocks per wave");
     const f32x4* d = reinterpret_cast<const f32x4*>(region);
     const f32x4 ml = d[2 * NE * 64 + lane];
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < QB; ++b) {
       const float la = row_sum(b), lb = ml[2 * b + 1];
       const float ma = la > 0.f ? m_ref[b] : ninf();
       const float mb = lb > 0.f ? ml[2 * b] : ninf();
@@ -796,7 +1085,7 @@ struct M16 {
   __device__ __forceinline__ void store_partial(__amdgpu_buffer_rsrc_t rpo, float* pml, int qw,
                                                 int S, float /*scale*/) {
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < QB; ++b) {
       const float lt = row_sum(b);
       const int q = qw + 16 * b + r16;
 #pragma unroll
@@ -820,7 +1109,8 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
                                                     char* smem) {
   constexpr int BN = Pol::BN;
   constexpr int NT = WAVES * 64;
-  constexpr int BM = WAVES * 32;
+  constexpr int RW = Pol::RW;              // query rows per wave (32, or 64 at one wave per SIMD)
+  constexpr int BM = WAVES * RW;
   constexpr int HD = Pol::HDIM;            // shadows the head_dim-128 defaults
   constexpr int ROW_BYTES = 2 * HD;        // HBM row
   constexpr int TILE_BYTES = BN * 256;     // LDS image: 256-B row slots at any head_dim
@@ -838,7 +1128,7 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
   const f16* Vh = p.v + head_off;
 
   const int q0 = qb * BM;
-  const int qw = q0 + wave * 32;  // first query row of this wave
+  const int qw = q0 + wave * RW;  // first query row of this wave
 
   int kv_lo = 0, kv_hi = CAUSAL ? min(q0 + BM, S) : S;
   if constexpr (SPLIT) {
@@ -900,7 +1190,7 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
     const int kv0 = kv_lo + j * BN;
     issue_loads(kv0 + BN);  // past kv_hi: zero bytes, no memory traffic
     // wave-uniform: does any key of this tile lie at/below some row of this wave?
-    if (!CAUSAL || kv0 <= qw + 31) {
+    if (!CAUSAL || kv0 <= qw + RW - 1) {
       const bool need_mask = (kv0 + BN > kv_hi) || (CAUSAL && kv0 + BN - 1 > qw);
       pol.template tile<CAUSAL>(kb, kb + TILE_BYTES, kv0, kv_hi, qw, c, need_mask);
     }
@@ -1446,5 +1736,156 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
 #endif
 #undef FA_KSTAMP
 }
+
+#ifdef FA_W4_EXPERIMENT  // tools/experiments/w4_spill_probe.sh (not in the library)
+// ---------------------------------------------------------------------------
+// W4 skeleton: 4 waves (one per SIMD), 64 query rows per wave, 256 rows per
+// workgroup.  Against the 8-wave ping-pong (32 rows per wave) every K/V
+// fragment read from LDS now feeds four MFMAs instead of two: half the LDS
+// bytes per FLOP, the ping-pong's measured largest non-MFMA cost.  With no
+// SIMD partner to hide the softmax behind, the wave overlaps it with its own
+// MFMAs by software pipelining across key tiles (iteration j):
+//   block 1: PV(j-1) first half      beside  row maxima of S(j)
+//   (rare, wave-uniform) move m_ref, shift S(j)
+//   block 2: PV(j-1) second half,    beside  P(j) = exp2(S(j)), cvt to fp16,
+//            QK^T(j+1)                        stage writes / next loads
+//   (rare) O, l *= alpha
+//   barrier
+// S(j+1) reuses the S(j) registers: the compiler orders each cvt before the
+// QK^T MFMA that overwrites its source.  O and l take alpha after PV(j-1)
+// because P(j-1) was relative to the old m_ref.
+// LDS: K and V double-buffered; stage j = (K_{j+2}, V_j) is loaded in
+// iteration j-1 (register staged) and written in iteration j.  K_{j+1} is
+// read in iteration j, V_{j-1} too, and each buffer written in iteration j
+// was last read in iteration j-1: one barrier per tile.
+// Causal: every tile up to the workgroup's diagonal runs on every wave (the
+// last wave needs them all and the barrier makes the others wait anyway);
+// tiles past a wave's rows are masked to -inf and contribute exp2 = 0.
+// ---------------------------------------------------------------------------
+template <class Pol, bool CAUSAL>
+__device__ __forceinline__ void attention_w4(const FwdParams& p, int bh, int qb, char* smem) {
+  constexpr int WAVES = 4;
+  constexpr int BN = Pol::BN;
+  constexpr int NT = WAVES * 64;
+  constexpr int RW = 16 * Pol::QB;           // query rows per wave
+  constexpr int BM = WAVES * RW;
+  constexpr int HD = Pol::HDIM;
+  constexpr int ROW_BYTES = 2 * HD;
+  constexpr int TILE_BYTES = BN * 256;
+  constexpr int NCH = (BN * (HD / 8)) / NT;  // 16-B chunks per thread per tile (K and V each)
+  static_assert((BN * (HD / 8)) % NT == 0, "tile chunks must divide evenly");
+  static_assert(Pol::QB == 4, "W4: 64 query rows per wave");
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int S = p.seq_len;
+
+  const size_t head_off = (size_t)bh * (size_t)S * HD;
+  const f16* Qh = p.q + head_off;
+  const f16* Kh = p.k + head_off;
+  const f16* Vh = p.v + head_off;
+
+  const int q0 = qb * BM;
+  const int qw = q0 + wave * RW;
+  const int kv_hi = CAUSAL ? min(q0 + BM, S) : S;
+  const int n = (kv_hi + BN - 1) / BN;
+
+  Pol pol;
+  pol.init(lane, p.c);
+  pol.issue_q(make_rsrc(Qh, S * ROW_BYTES), qw);
+
+  auto kbuf = [&](int x) { return smem + (x & 1) * TILE_BYTES; };
+  auto vbuf = [&](int x) { return smem + (2 + (x & 1)) * TILE_BYTES; };
+  const int kr0 = pol.k_stage_row(wave), kc = pol.k_stage_ch();
+  const int vr0 = pol.v_stage_row(wave), vc = pol.v_stage_ch();
+  f16x8 kst[NCH], vst[NCH];
+  // stage j = (K_{j+2}, V_j); rows at/after kv_hi and tiles < 0 read as 0
+  auto issue_stage = [&](int j) {
+    const int kb_row = (j + 2) * BN, vb_row = j * BN;
+    const auto rk = make_rsrc(Kh + (size_t)min(kb_row, S) * HD, (kv_hi - kb_row) * ROW_BYTES);
+    const auto rv = make_rsrc(Vh + (size_t)max(vb_row, 0) * HD,
+                              vb_row < 0 ? 0 : (kv_hi - vb_row) * ROW_BYTES);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      kst[i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
+      vst[i] = buf_load16(rv, (vr0 + Pol::RPW * WAVES * i) * ROW_BYTES + vc * 16);
+    }
+  };
+  auto write_stage = [&](int j) {
+    char* kb = kbuf(j + 2);
+    char* vb = vbuf(j);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      *reinterpret_cast<f16x8*>(kb + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = kst[i];
+      *reinterpret_cast<f16x8*>(vb + Pol::v_lds(vr0 + Pol::RPW * WAVES * i, vc)) = vst[i];
+    }
+  };
+
+  // prologue: Q, K_0 and stage -1 (K_1) in flight together
+  {
+    const auto rk = make_rsrc(Kh, kv_hi * ROW_BYTES);
+    f16x8 k0[NCH];
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      k0[i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
+    issue_stage(-1);
+    __builtin_amdgcn_sched_barrier(0);  // all prologue loads issued first (attention_tile_loop)
+    pol.scale_q();
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      *reinterpret_cast<f16x8*>(kbuf(0) + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = k0[i];
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * NCH));  // Q, K_0 retired; stage -1 may fly
+  __syncthreads();
+
+  // iteration -1: QK^T(0), stage -1 written, stage 0 loads issued
+  write_stage(-1);
+  issue_stage(0);
+  pol.qk(kbuf(0));
+  __syncthreads();
+
+  // one pipelined iteration (j = the softmax tile), P buffer PB = j & 1:
+  //   PV(j-1) beside exp/cvt of S(j); O, l *= alpha(j) after PV(j-1) (rare);
+  //   then QK^T(j+1) chain-major beside the stage traffic, and the row
+  //   maxima / rare rescale bookkeeping of S(j+1).  One body per P buffer;
+  //   the mask is a runtime branch around the masking code only.
+  auto need_mask = [&](int j) {
+    const int kv0 = j * BN;
+    return (kv0 + BN > kv_hi) || (CAUSAL && kv0 + BN - 1 > qw);
+  };
+  bool resc = false;
+  auto iter = [&](int j, auto pb_c) {
+    constexpr int PB = decltype(pb_c)::value;
+    if (j >= 1) pol.template pv_buf<PB ^ 1>(vbuf(j - 1));
+    pol.template exp_cvt<PB>();
+    if (resc) pol.sm_alpha();  // alpha(j): O holds PV(..j-1) at the old m_ref
+    resc = false;
+    if (j + 1 < n) pol.qk_cm(kbuf(j + 1));
+    write_stage(j);
+    issue_stage(j + 1);
+    if (j + 1 < n) {
+      if (pol.template sm_max<CAUSAL>((j + 1) * BN, kv_hi, qw, need_mask(j + 1))) resc = pol.sm_shift();
+    }
+    __syncthreads();
+  };
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  // S(0): row maxima and first m_ref (the first shift only centres m_ref: O is zero)
+  if (n > 0 && pol.template sm_max<CAUSAL>(0, kv_hi, qw, need_mask(0))) pol.sm_shift();
+  int j = 0;
+  for (; j + 1 < n; j += 2) {
+    iter(j, P0{});
+    iter(j + 1, P1{});
+  }
+  if (j < n) {
+    iter(j, P0{});
+    pol.template pv_buf<0>(vbuf(j));
+  } else if (n > 0) {
+    pol.template pv_buf<1>(vbuf(j - 1));
+  }
+  pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);
+}
+#endif  // FA_W4_EXPERIMENT
 
 }  // namespace fa

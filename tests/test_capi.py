@@ -78,12 +78,13 @@ def test_config_table():
             assert c.block_m == 8 * c.waves
             assert c.lds_bytes == 4 * 2 * c.block_n * 256
             continue
-        assert c.block_m == 32 * c.waves
+        # 64 query rows per wave (one wave per SIMD) or 32
+        assert c.block_m == (64 if "_w4x64_" in c.name else 32) * c.waves
         # K and V image buffers of 256-B row slots: double-buffered, or three
         # rotating buffers each for the LDS-DMA configs
         nbuf = 3 if "_dma_" in c.name else 2
         need = 2 * nbuf * c.block_n * 256
-        if "_persistent_" in c.name and "_dma_" not in c.name and not c.causal:
+        if "_pingpong_persistent_" in c.name and "_dma_" not in c.name and not c.causal:
             need = max(need, 4 * 17 * 64 * 16)  # room for the KV-pair tail halves
         assert c.lds_bytes == need <= 160 * 1024
     # every (waves, bn) non-split config exists for both masks
