@@ -197,12 +197,37 @@ __global__ __launch_bounds__(WAVES * 64, QB == 4 ? 1 : 2) void fa_fwd_f16_persis
 #endif
   const int full = L / C, tail = L - full * C;
   const bool split_tail = kTailSplit && tail > 0 && 2 * tail <= C;
-  const int rounds = split_tail ? full : (L + C - 1) / C;
+  // Causal pair order: CU lcu runs the two query blocks (nqb-1-p, p) of one
+  // head back to back -- the heavy one in round 2R, the light one in round
+  // 2R+1 -- so every CU costs exactly nqb+1 key tiles per pair of rounds and
+  // the pairs' heavy items co-start: the XCD's CUs walk one or two heads'
+  // K/V tiles in lockstep (heavy items) or as a one-tile-apart staircase
+  // (light items), which the 4 MB L2 holds.  The snake over rank bands
+  // below balances the same way but mixes heads and ranks in a round, and
+  // after the first round its items start staggered (2.2-3.5x the
+  // algorithmic HBM bytes at B=1 S=8192-16384, profiles/r01_tier_pmc.txt).
+  // Pairs cut that to 1.38-1.39x at equal speed; with many heads per XCD the
+  // band-16 snake co-starts whole heads and fetches less (B=64 S=4096: 1.07x
+  // vs 1.41x), so pairs replace only the plain heaviest-first order (band 1,
+  // <= 64 heads; profiles/r02_causal_pairs_{ab,traffic}.jsonl).
+#ifndef FA_CAUSAL_PAIRS
+#define FA_CAUSAL_PAIRS 1
+#endif
+  const bool pairs =
+      FA_CAUSAL_PAIRS && CAUSAL && items.affine && (p.nqb & 1) == 0 && p.band == 1;
+  const int npairs = items.hx * (p.nqb >> 1);
+  const int rounds = pairs ? 2 * ((npairs + C - 1) / C) : split_tail ? full : (L + C - 1) / C;
   for (int r = 0; r < rounds; ++r) {
-    const int pos = r * C + ((r & 1) ? (C - 1 - lcu) : lcu);
-    if (pos < L) {
+    const int pos = pairs ? (r >> 1) * C + lcu : r * C + ((r & 1) ? (C - 1 - lcu) : lcu);
+    if (pos < (pairs ? npairs : L)) {
       int bh, qb;
-      item_of(pos, bh, qb);
+      if (pairs) {
+        const int half = p.nqb >> 1, lh = pos / half, pp = pos - lh * half;
+        bh = x + 8 * lh;
+        qb = (r & 1) ? pp : p.nqb - 1 - pp;
+      } else {
+        item_of(pos, bh, qb);
+      }
 #ifdef FA_STAMPS
       const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
       const unsigned long long c_start = __builtin_amdgcn_s_memtime();
