@@ -991,15 +991,6 @@ struct M16 {
     softmax<CAUSAL>(kv0, kv_hi, qw, c_, need_mask);
     pv(vb);
   }
-  // Speculative softmax (one wave per SIMD): QK^T chain-major, and each S
-  // column block cb is exponentiated against the current m_ref (P to fp16)
-  // as soon as its four chains are done, beside the remaining chains'
-  // MFMAs -- no row-max reduction or branch inside the MFMA stream.  A block
-  // whose partial max exceeds RESCALE_LOG2 only sets a flag; if any row of
-  // the tile grew past it (rare; always on the first tile), the full softmax
-  // recomputes P from the untouched S with the moved m_ref, exactly as the
-  // non-speculative path would.  Masked tiles (diagonal, ragged end) take the
-  // same recompute, which applies the mask: one body, one rare branch.
 
   __device__ __forceinline__ float row_sum(int b) const {
 #ifdef FA_ROWSUM_VALU
