@@ -39,6 +39,12 @@ SHAPES = [  # (label, batch, heads, seq, causal)
     ("cfg4_b8_s4096_causal_shard", 8, 32, 4096, True),   # one GPU's shard of config 5 at N=8
     ("headline_b64_s4096_causal", 64, 32, 4096, True),
     ("s256_b16_noncausal", 16, 32, 256, False),
+    # non-dispatched tile configs (BM, BN, waves) on the same shapes: the
+    # 64-rows-per-wave W4x64 tiers and the per-item 8-wave ping-pong
+    ("w4x64_s8192_noncausal", 1, 32, 8192, False, "bm256_bn64_w4x64_m16_persistent_noncausal"),
+    ("w4x64_s8192_causal", 1, 32, 8192, True, "bm256_bn64_w4x64_m16_persistent_causal"),
+    ("w4x64_headline_b64_s4096_causal", 64, 32, 4096, True, "bm256_bn64_w4x64_m16_persistent_causal"),
+    ("pingpong_item_s8192_causal", 1, 32, 8192, True, "bm256_bn64_w8_m16_pingpong_causal"),
 ]
 ITERS = 6
 PEAK = 2516.6  # TFLOP/s, 256 CU x 2.4 GHz x 4096 FLOP/clk/CU
@@ -54,24 +60,26 @@ def run(time_it):
 
     g = torch.Generator(device="cuda")
     g.manual_seed(7)
-    for label, b, h, s, causal in SHAPES:
+    names = {c.name: c.id for c in fa.configs()}
+    for label, b, h, s, causal, *forced in SHAPES:
         shape = (b, h, s, 128)
         q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5, generator=g)
                    for _ in range(3))
         o = torch.empty_like(q)
-        cfg = fa.select_config(b, h, s, causal)
+        cfg = names[forced[0]] if forced else fa.select_config(b, h, s, causal)
+        fwd = lambda: fa.flash_attention_fwd(q, k, v, causal, out=o, config=cfg)
         flops = fa.attention_flops(b, h, s, 128, causal)
         torch.cuda.synchronize()
         if time_it:
             for _ in range(3):
-                fa.flash_attention_fwd(q, k, v, causal, out=o)
+                fwd()
             n = 50 if flops < 1e12 else 10
             best = []
             for _ in range(3):
                 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 st.record()
                 for _ in range(n):
-                    fa.flash_attention_fwd(q, k, v, causal, out=o)
+                    fwd()
                 en.record()
                 en.synchronize()
                 best.append(st.elapsed_time(en) / n)
@@ -82,7 +90,7 @@ def run(time_it):
                               "alg_bytes": 8.0 * b * h * s * 128}), flush=True)
         else:
             for _ in range(ITERS):
-                fa.flash_attention_fwd(q, k, v, causal, out=o)
+                fwd()
             torch.cuda.synchronize()
         del q, k, v, o
 
@@ -114,7 +122,7 @@ def summary(timing_jsonl, mfma_dir, fetch_dir, write_dir, out):
     # a launch may be one kernel (all dispatched tiers are single-kernel)
     assert len(dur) == ITERS * len(SHAPES), (len(dur), ITERS * len(SHAPES))
     rows = []
-    for i, (label, b, h, s, causal) in enumerate(SHAPES):
+    for i, (label, b, h, s, causal, *_) in enumerate(SHAPES):
         sl = slice(i * ITERS + 1, (i + 1) * ITERS)  # drop the first (cold) launch
         mean = lambda xs: sum(xs[sl]) / len(xs[sl])
         busy, grbm, nmf = mean(m["SQ_VALU_MFMA_BUSY_CYCLES"]), mean(m["GRBM_GUI_ACTIVE"]), mean(m["SQ_INSTS_MFMA"])
