@@ -166,6 +166,16 @@ __device__ __forceinline__ f16x4 lds_read_tr(const char* base, int off) {
 
 __device__ __forceinline__ float ninf() { return -__builtin_inff(); }
 
+// 32-bit LDS address of a pointer into the workgroup's shared memory
+__device__ __forceinline__ int lds_addr(const void* p) {
+  return (int)(unsigned)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
+}
+
+#ifndef FA_W4_TILE_INC
+#define FA_W4_TILE_INC "fa_w4_tile_asm.inc"  // diagnostic builds swap in a variant
+#endif
+#include FA_W4_TILE_INC  // w4_tile_asm: hand-scheduled W4x64 tile body
+
 #ifdef FA_STAMPS
 // diagnostic build only (lib/libfa_mi355x_stamps.so): per-wave cycles spent in
 // [MFMA block, barrier after it, softmax block, barrier after it, LDS tile write], summed over
@@ -987,6 +997,20 @@ struct M16 {
   template <bool CAUSAL>
   __device__ __forceinline__ void tile(const char* kb, const char* vb, int kv0, int kv_hi, int qw,
                                        float c_, bool need_mask) {
+#ifdef FA_W4_TILE_ASM  // opt-in: measured level with (non-causal) or 2-4 % below (causal) the plain body
+    if constexpr (kAsm) {
+      // common case: the hand-scheduled tile body (tools/gen_w4_tile_asm.py);
+      // masked tiles, the first tile and a row max past RESCALE_LOG2 (rare)
+      // take the plain path below, which recomputes S from the same LDS tile
+      if (!need_mask && have_ref) {
+        const int kl = lds_addr(kb), vl = lds_addr(vb);
+        const int ka[4] = {kl + kaddr[0], kl + kaddr[1], kl + kaddr[2], kl + kaddr[3]};
+        const int va[2] = {vl + vaddr[0], vl + vaddr[1]};
+        const tx8 ones = {(T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f};
+        if (!w4_tile_asm(acc, lacc, qf, m_ref, ka, va, ones)) return;
+      }
+    }
+#endif
     qk(kb);
     softmax<CAUSAL>(kv0, kv_hi, qw, c_, need_mask);
     pv(vb);
@@ -1183,19 +1207,47 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
   __syncthreads();
 
   const float c = p.c;
+#ifdef FA_STAMPS
+  // diagnostic build: [0] tile body, [1] staged-load wait + LDS writes,
+  // [2] barrier, [3] load issue; [6] tiles, [7] prologue (per item)
+  unsigned long long st_acc[12] = {}, sa, sb, sc, sd, se;
+  st_acc[9] = 1;
+#define FA_TSTAMP(v)                                                          \
+  do {                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+  } while (0)
+#else
+#define FA_TSTAMP(v) \
+  do {               \
+  } while (0)
+#endif
   auto step = [&](int j, auto buf_c) {
     constexpr int BUF = decltype(buf_c)::value;
     char* kb = smem + BUF * 2 * TILE_BYTES;
     char* kb_next = smem + (BUF ^ 1) * 2 * TILE_BYTES;
     const int kv0 = kv_lo + j * BN;
+    FA_TSTAMP(sa);
     issue_loads(kv0 + BN);  // past kv_hi: zero bytes, no memory traffic
+    FA_TSTAMP(sb);
     // wave-uniform: does any key of this tile lie at/below some row of this wave?
     if (!CAUSAL || kv0 <= qw + RW - 1) {
       const bool need_mask = (kv0 + BN > kv_hi) || (CAUSAL && kv0 + BN - 1 > qw);
       pol.template tile<CAUSAL>(kb, kb + TILE_BYTES, kv0, kv_hi, qw, c, need_mask);
     }
+    FA_TSTAMP(sc);
     write_lds(kb_next);
+    FA_TSTAMP(sd);
     __syncthreads();
+    FA_TSTAMP(se);
+#ifdef FA_STAMPS
+    st_acc[0] += sc - sb;
+    st_acc[1] += sd - sc;
+    st_acc[2] += se - sd;
+    st_acc[3] += sb - sa;
+    st_acc[6] += 1;
+#endif
   };
   int j = 0;
   for (; j + 1 < ntiles; j += 2) {
@@ -1203,6 +1255,11 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
     step(j + 1, std::integral_constant<int, 1>{});
   }
   if (j < ntiles) step(j, std::integral_constant<int, 0>{});
+#ifdef FA_STAMPS
+  if (lane == 0 && blockIdx.x < 64)
+    for (int i = 0; i < 12; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
+#endif
+#undef FA_TSTAMP
 
   if constexpr (!SPLIT) {
     pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);
