@@ -166,6 +166,17 @@ __device__ __forceinline__ f16x4 lds_read_tr(const char* base, int off) {
 
 __device__ __forceinline__ float ninf() { return -__builtin_inff(); }
 
+// Cache policy of the O stores: sc1 (write-through; the line leaves the
+// XCD's L2 with the store).  O is written once and never re-read by the
+// kernel; on the short tiers, where every workgroup stores at the end of the
+// launch, write-through drains the tail faster: B=1 H=32 S=512 non-causal
+// 300 -> 316, S=1024 causal 392 -> 415 TFLOP/s; nt +1-3 %; the persistent
+// tier is level (+-0.3 %) (profiles/r02_ab_o_store_policy.jsonl).  Buffer
+// store aux bits: 2 = nt, 16 = sc1.
+#ifndef FA_O_STORE_AUX
+#define FA_O_STORE_AUX 16
+#endif
+
 // 32-bit LDS address of a pointer into the workgroup's shared memory
 __device__ __forceinline__ int lds_addr(const void* p) {
   return (int)(unsigned)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
@@ -1063,7 +1074,7 @@ struct M16 {
           Y[dw] = r[1];
         }
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{X[0], X[1], Y[0], Y[1]}, ro,
-                                               rowb + 2 * (32 * ep + dlane), 0, 0);
+                                               rowb + 2 * (32 * ep + dlane), 0, FA_O_STORE_AUX);
       }
 #endif
     }
