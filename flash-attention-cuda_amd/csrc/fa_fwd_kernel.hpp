@@ -1479,7 +1479,30 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   do {              \
   } while (0)
 #endif
-  for (int k = 0; k <= n; ++k) {
+  // The last MFMA phase (k = n: the PV of tile n-1 alone) is peeled so each
+  // group's O leaves right after it -- group A's a half-step before group
+  // B's, so B's stores no longer queue behind A's (round-1 stamps: group B
+  // epilogue 6.2k cycles vs A 2.2k per item); the barriers after it only
+  // keep the LDS hand-off order for the next item.  Causal only: +1-3 % on
+  // the causal persistent shapes, while the non-causal build took more SGPR
+  // spills (35 -> 42) and was level to 4 % slower
+  // (profiles/r02_ab_early_o_store.jsonl).  FA_LATE_STORE: the round-1 order
+  // (both groups store after the final barrier).
+#ifdef FA_LATE_STORE
+  constexpr bool kEarlyStore = false;
+#else
+  constexpr bool kEarlyStore = CAUSAL;
+#endif
+  auto store_out = [&]() {
+    if constexpr (!SPLIT) {
+      pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);
+    } else {
+      const size_t prow0 = ((size_t)split * p.bh + bh) * (size_t)S;
+      pol.store_partial(make_rsrc(p.part_o + prow0 * HD, S * HD * 4), p.part_ml + prow0 * 2, qw, S,
+                        p.scale);
+    }
+  };
+  for (int k = 0; k < (kEarlyStore ? n : n + 1); ++k) {
     const int t = k + grp;
     FA_STAMP(st0);
     if (!kIssueInSm && t < n) issue_tile(t);
@@ -1522,19 +1545,19 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     st_acc[6] += 1;
 #endif
   }
+  if constexpr (kEarlyStore) {
+    mfma_block(n);  // PV of tile n-1 (no tile n: the softmax half-step is empty)
+    store_out();
+    __syncthreads();
+    __syncthreads();
+  }
   if (grp == 0) __syncthreads();
   if constexpr (PRIO && FA_PRIO_MODE == 2) __builtin_amdgcn_s_setprio(0);
 #ifdef FA_STAMPS
   const unsigned long long t_le = __builtin_amdgcn_s_memtime();
 #endif
 
-  if constexpr (!SPLIT) {
-    pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);
-  } else {
-    const size_t prow0 = ((size_t)split * p.bh + bh) * (size_t)S;
-    pol.store_partial(make_rsrc(p.part_o + prow0 * HD, S * HD * 4), p.part_ml + prow0 * 2, qw, S,
-                      p.scale);
-  }
+  if constexpr (!kEarlyStore) store_out();
 #ifdef FA_STAMPS
   __builtin_amdgcn_s_waitcnt(0);  // stores issued and retired
   st_acc[8] = __builtin_amdgcn_s_memtime() - t_le;
