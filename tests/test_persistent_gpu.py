@@ -57,7 +57,26 @@ SHAPES = [
     (4, 50, 64),     # single-tile items (n = 1)
     (1, 7, 4096),    # fewer heads than XCD groups
     (1, 2, 4096),    # 2 heads: non-affine split of the items over all 8 XCDs
+    # causal work orders (fa_fwd.hip persistent kernel): pair order at <= 64
+    # heads with an even number of query blocks, else the rank-band snake
+    (1, 32, 2048),   # pairs: 8 query blocks, 4 heads per XCD group
+    (1, 64, 1536),   # pairs at the 64-head boundary, 6 query blocks
+    (1, 16, 1280),   # odd query-block count (5): band-1 snake fallback
+    (1, 72, 1024),   # 72 heads (> 64): band-16 snake, 4 query blocks
 ]
+
+
+def _nc_tail_split(kind, b, h, s, causal, cus=256):
+    """The persistent non-causal register-staged kernel runs an XCD's last
+    round as KV-pair halves when it holds <= C/2 items (fa_fwd.hip): those
+    rows are not bit-identical to the ping-pong (key split + LSE merge)."""
+    if causal or kind != "persistent":
+        return False
+    bh, nqb = b * h, (s + 255) // 256
+    per_xcd = (bh // 8) * nqb if bh % 8 == 0 else (bh * nqb + 7) // 8
+    c = min(cus // 8, per_xcd)
+    tail = per_xcd - (per_xcd // c) * c
+    return 0 < tail and 2 * tail <= c
 
 
 @pytest.mark.parametrize("causal", [False, True])
@@ -71,7 +90,11 @@ def test_persistent_bit_identical(kind, shape, causal):
     out_base = fa.flash_attention_fwd(q, k, v, causal=causal, config=base_id)
     out = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(kind)[causal])
     torch.cuda.synchronize()
-    assert torch.equal(out, out_base)
+    cus = torch.cuda.get_device_properties(q.device).multi_processor_count
+    if _nc_tail_split(kind, b, h, s, causal, cus):
+        assert (out.float() - out_base.float()).abs().max().item() <= TOL
+    else:
+        assert torch.equal(out, out_base)
     # sampled heads against the oracle: first, last, and one in the middle
     for flat in sorted({0, b * h // 2, b * h - 1}):
         bi, hi = divmod(flat, h)
