@@ -173,6 +173,21 @@ __device__ __forceinline__ float ninf() { return -__builtin_inff(); }
 // 300 -> 316, S=1024 causal 392 -> 415 TFLOP/s; nt +1-3 %; the persistent
 // tier is level (+-0.3 %) (profiles/r02_ab_o_store_policy.jsonl).  Buffer
 // store aux bits: 2 = nt, 16 = sc1.
+// head_dim 64 non-causal ping-pong schedule: the causal one (next tile's
+// loads issued in the MFMA phase, written at the start of the softmax phase,
+// O stored right after the last PV).  With half the MFMAs per tile the MFMA
+// phase is the short one at d64, the reverse of d128; +15-20 % at S=2048-16384
+// fp16 and bf16, bit-identical (profiles/r02_ab_d64_noncausal_sched.jsonl).
+// The knobs restore the d128 non-causal choices (1, 0, 0) for A/B.
+#ifndef FA_NC_D64_ISSUE_IN_SM
+#define FA_NC_D64_ISSUE_IN_SM 0
+#endif
+#ifndef FA_NC_D64_WRITE_EARLY
+#define FA_NC_D64_WRITE_EARLY 1
+#endif
+#ifndef FA_NC_D64_EARLY_STORE
+#define FA_NC_D64_EARLY_STORE 1
+#endif
 #ifndef FA_O_STORE_AUX
 #define FA_O_STORE_AUX 16
 #endif
@@ -1346,12 +1361,13 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   // phase (causal), or at the end of the softmax phase, by the wave whose
   // phase is the shorter one (non-causal: +2 % at S=8192; causal: -5 %, its
   // masked/inactive tiles shorten the MFMA phases instead)
-  constexpr bool kIssueInSm = DMA || !CAUSAL;  // DMA: legal with three buffers
+  constexpr bool kIssueInSm =
+      DMA || (!CAUSAL && (Pol::HDIM == 128 || FA_NC_D64_ISSUE_IN_SM));  // DMA: three buffers
   // where a tile is written to LDS: at the start of the softmax phase (beside
   // the partner's MFMAs; causal: +0.3-0.7 % A/B) or at its end (non-causal:
   // early was -0.8 %, its loads are issued in the softmax phase and need it
   // to land)
-  constexpr bool kWriteEarly = CAUSAL && !DMA;
+  constexpr bool kWriteEarly = !DMA && (CAUSAL || (Pol::HDIM == 64 && FA_NC_D64_WRITE_EARLY));
   static_assert(!DMA || Pol::HDIM == 128, "LDS-DMA path: head_dim 128");
 
 #ifdef FA_STAMPS
@@ -1491,7 +1507,7 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
 #ifdef FA_LATE_STORE
   constexpr bool kEarlyStore = false;
 #else
-  constexpr bool kEarlyStore = CAUSAL;
+  constexpr bool kEarlyStore = CAUSAL || (Pol::HDIM == 64 && FA_NC_D64_EARLY_STORE);
 #endif
   auto store_out = [&]() {
     if constexpr (!SPLIT) {

@@ -23,6 +23,7 @@ ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--iters", type=int, default=30)
 ap.add_argument("--env", default="", help="label only")
 ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"])
+ap.add_argument("--head-dim", type=int, default=128, choices=[64, 128])
 ap.add_argument("--data", default="uniform", choices=["uniform", "zeros", "small"],
                 help="uniform[-0.5,0.5] (default), all zeros, or uniform[-0.01,0.01]")
 ap.add_argument("--libs", default="", help="comma list of library variants: '' = libfa_mi355x.so, "
@@ -30,7 +31,7 @@ ap.add_argument("--libs", default="", help="comma list of library variants: '' =
 a = ap.parse_args()
 g = torch.Generator(device="cuda")
 g.manual_seed(3)
-shape = (a.batch, a.heads, a.seq, 128)
+shape = (a.batch, a.heads, a.seq, a.head_dim)
 dt = torch.bfloat16 if a.dtype == "bf16" else torch.float16
 q, k, v = (torch.empty(shape, dtype=dt, device="cuda").uniform_(-0.5, 0.5, generator=g)
            for _ in range(3))
@@ -48,7 +49,7 @@ for var in a.libs.split(","):
     fa.LIB_PATH = os.path.join(HERE, "lib", "libfa_mi355x%s.so" % ("_" + var if var else ""))
     libs[var] = fa.load_library()
 cids = [(var, int(x)) for x in a.configs.split(",") for var in libs]
-flops = fa.attention_flops(a.batch, a.heads, a.seq, 128, a.causal)
+flops = fa.attention_flops(a.batch, a.heads, a.seq, a.head_dim, a.causal)
 res = {c: [] for c in cids}
 for c in cids:  # warm
     fa._lib = libs[c[0]]
@@ -67,6 +68,6 @@ for _ in range(a.rounds):
         res[c].append(flops / (st.elapsed_time(en) / a.iters / 1e3) / 1e12)
 names = {c.id: c.name for c in fa.configs()}
 for c in cids:
-    print(json.dumps({"config": names[c[1]], "lib": c[0] or "base", "env": a.env, "seq": a.seq, "batch": a.batch, "heads": a.heads, "data": a.data, "causal": a.causal,
+    print(json.dumps({"config": names[c[1]], "lib": c[0] or "base", "env": a.env, "seq": a.seq, "head_dim": a.head_dim, "batch": a.batch, "heads": a.heads, "data": a.data, "causal": a.causal,
                       "median_tflops": round(statistics.median(res[c]), 1),
                       "min_tflops": round(min(res[c]), 1), "max_tflops": round(max(res[c]), 1)}))

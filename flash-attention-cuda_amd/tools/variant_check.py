@@ -1,7 +1,7 @@
 """Bit-identity check of a library variant against the product library on the
 dispatched tiers (same inputs, same config id): a variant that only changes
 scheduling or data movement must reproduce the product's output bit for bit.
-usage: python tools/variant_check.py VARIANT"""
+usage: python tools/variant_check.py VARIANT [HEAD_DIM]"""
 import os
 import sys
 
@@ -12,6 +12,7 @@ import fa_mi355x as fa  # noqa: E402
 
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 var = sys.argv[1]
+hd = int(sys.argv[2]) if len(sys.argv) > 2 else 128
 libs = {}
 for v in ("", var):
     fa._lib = None
@@ -24,7 +25,7 @@ g.manual_seed(11)
 bad = 0
 for dt in (torch.float16, torch.bfloat16):
     for b, h, s in SHAPES:
-        q, k, v = (torch.empty((b, h, s, 128), dtype=dt, device="cuda").uniform_(-0.5, 0.5, generator=g)
+        q, k, v = (torch.empty((b, h, s, hd), dtype=dt, device="cuda").uniform_(-0.5, 0.5, generator=g)
                    for _ in range(3))
         for causal in (False, True):
             outs = []
@@ -34,7 +35,7 @@ for dt in (torch.float16, torch.bfloat16):
             torch.cuda.synchronize()
             same = torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
             cfg = fa.configs()[fa.select_config(b, h, s, causal) if dt == torch.float16 else 0].name
-            print(f"{str(dt):15s} B={b} H={h} S={s} causal={causal} {cfg}: "
+            print(f"{str(dt):15s} D={hd} B={b} H={h} S={s} causal={causal} {cfg}: "
                   f"{'bit-identical' if same else 'DIFFERENT max %.3g' % (outs[0].float() - outs[1].float()).abs().max().item()}",
                   flush=True)
             bad += not same
