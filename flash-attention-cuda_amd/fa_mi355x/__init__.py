@@ -185,6 +185,9 @@ def kernel_attrs(config_id: int) -> dict:
     return {f: getattr(ka, f) for f, _ in _KernelAttrs._fields_}
 
 
+_DTYPES_16 = ()  # (torch.float16, torch.bfloat16) once torch is imported (lazily)
+
+
 def _stream_handle(stream, device=None) -> Optional[int]:
     """Raw hipStream_t of `stream` (None: torch's current stream on `device`)."""
     import torch
@@ -197,6 +200,25 @@ def _stream_handle(stream, device=None) -> Optional[int]:
 
 
 def _check_qkvo(q, k, v, out):
+    """Raise FlashAttentionError unless q, k, v, out are contiguous [B,H,S,D]
+    device tensors of one 16-bit dtype, shape and device.  The common case is
+    one short-circuit expression (a short launch's host cost is mostly this
+    wrapper, tools/host_overhead.py); the per-tensor loop names the culprit."""
+    global _DTYPES_16
+    if not _DTYPES_16:
+        import torch
+
+        _DTYPES_16 = (torch.float16, torch.bfloat16)
+    dt, sh, dv = q.dtype, q.shape, q.device
+    if (q.is_cuda and len(sh) == 4 and dt in _DTYPES_16 and k.dtype is dt and v.dtype is dt
+            and out.dtype is dt and k.shape == sh and v.shape == sh and out.shape == sh
+            and k.device == dv and v.device == dv and out.device == dv and q.is_contiguous()
+            and k.is_contiguous() and v.is_contiguous() and out.is_contiguous()):
+        return
+    _check_qkvo_each(q, k, v, out)
+
+
+def _check_qkvo_each(q, k, v, out):
     import torch
 
     if q.dtype not in (torch.float16, torch.bfloat16):
@@ -231,19 +253,26 @@ def flash_attention_fwd(q, k, v, causal: bool = False, out=None, config: Optiona
         out = torch.empty_like(q)
     _check_qkvo(q, k, v, out)
     b, h, s, d = q.shape
-    lib = load_library()
-    args = (ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(k.data_ptr()),
-            ctypes.c_void_p(v.data_ptr()), ctypes.c_void_p(out.data_ptr()), b, h, s, d,
-            int(bool(causal)))
-    bf16 = q.dtype == torch.bfloat16
+    lib = _lib or load_library()
+    bf16 = q.dtype is torch.bfloat16
+    dev = q.device.index
+    if stream is None:
+        st = torch._C._cuda_getCurrentRawStream(dev)
+    else:
+        st = stream if isinstance(stream, int) else stream.cuda_stream
+    args = (q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), b, h, s, d, int(bool(causal)))
+    if config is None:
+        fn = lib.fa_fwd_bf16 if bf16 else lib.fa_fwd_f16
+    else:
+        fn = lib.fa_fwd_bf16_config if bf16 else lib.fa_fwd_f16_config
+        args += (int(config),)
     # the C side launches on (and sizes for) the current device: make it q's
-    with torch.cuda.device(q.device):
-        st = ctypes.c_void_p(_stream_handle(stream, q.device))
-        if config is None:
-            _check((lib.fa_fwd_bf16 if bf16 else lib.fa_fwd_f16)(*args, st))
-        else:
-            _check((lib.fa_fwd_bf16_config if bf16 else lib.fa_fwd_f16_config)(*args, int(config),
-                                                                                st))
+    if dev == torch._C._cuda_getDevice():
+        rc = fn(*args, st)
+    else:
+        with torch.cuda.device(dev):
+            rc = fn(*args, st)
+    _check(rc)
     return out
 
 

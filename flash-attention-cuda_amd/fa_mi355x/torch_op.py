@@ -5,11 +5,16 @@ rank 3: the wrapper that puts the kernel beside PyTorch SDPA on one box).
     o = torch.ops.fa_mi355x.fwd(q, k, v, causal=True)
 
 ``q, k, v``: fp16 or bf16 ``[B, H, S, D]`` (D = 128 or 64) tensors on the GPU (BHSD, the
-reference layout, flash_attention.cu:119-122); returns a new tensor of the same shape and dtype.  The op is registered with ``torch.library.custom_op`` so it is
-opaque to ``torch.compile`` (a fake/meta implementation supplies the output
-shape) and launches on the current HIP stream, so it can be captured in a
-HIP graph.  It calls the same C ABI as every other entry point; there is no
-CPU or eager fallback (a CPU tensor raises).
+reference layout, flash_attention.cu:119-122); returns a new tensor of the same shape and dtype.
+The schema is defined with ``torch.library.Library`` and the kernel registered
+for the CUDA dispatch key directly (``custom_op``'s extra dispatch layers cost
+3.7 us more per call than this registration, 12.2 vs 8.5 us host time on a
+short launch, tools/host_overhead.py); a fake (meta) implementation supplies
+the output shape, so the op is opaque to ``torch.compile``, and it launches on
+the current HIP stream, so it can be captured in a HIP graph.  It calls the
+same C ABI as every other entry point; there is no CPU or eager fallback (a
+CPU tensor raises ValueError).  Forward only: no autograd formula is
+registered.
 """
 from __future__ import annotations
 
@@ -19,16 +24,26 @@ from . import flash_attention_fwd
 
 OP_NAME = "fa_mi355x::fwd"
 
+_LIB = torch.library.Library("fa_mi355x", "DEF")
+_LIB.define("fwd(Tensor q, Tensor k, Tensor v, bool causal=False) -> Tensor")
 
-@torch.library.custom_op(OP_NAME, mutates_args=())
-def fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = False) -> torch.Tensor:
-    if not (q.is_cuda and k.is_cuda and v.is_cuda):
-        raise ValueError("fa_mi355x::fwd needs GPU tensors (no CPU path)")
+
+def _fwd_gpu(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = False) -> torch.Tensor:
     return flash_attention_fwd(q.contiguous(), k.contiguous(), v.contiguous(), causal=causal)
 
 
-@fwd.register_fake
+def _fwd_cpu(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = False) -> torch.Tensor:
+    raise ValueError("fa_mi355x::fwd needs GPU tensors (no CPU path)")
+
+
 def _fwd_fake(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = False) -> torch.Tensor:
     torch._check(q.dim() == 4 and q.shape[-1] in (64, 128), lambda: "expected [B, H, S, 64|128]")
     torch._check(q.dtype in (torch.float16, torch.bfloat16), lambda: "expected fp16 or bf16")
     return torch.empty_like(q, memory_format=torch.contiguous_format)
+
+
+_LIB.impl("fwd", _fwd_gpu, "CUDA")
+_LIB.impl("fwd", _fwd_cpu, "CPU")
+torch.library.register_fake(OP_NAME, _fwd_fake, lib=_LIB)
+
+fwd = torch.ops.fa_mi355x.fwd
