@@ -492,6 +492,9 @@ static int check_args(const void* q, const void* k, const void* v, const void* o
   if (batch < 0 || heads < 0 || seq_len < 0 || head_dim < 0) return FA_ERR_BAD_SHAPE;
   if (head_dim != 128 && head_dim != 64) return FA_ERR_UNSUPPORTED_HEAD_DIM;
   if ((long long)batch * heads > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
+  // a head's rows are addressed through one buffer resource whose byte range
+  // (S * 2 * head_dim) is a 32-bit int: S <= 8388607 at head_dim 128
+  if ((long long)seq_len * 2 * head_dim > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
   if (!q || !k || !v || !o) return FA_ERR_NULL_POINTER;
   return FA_OK;
@@ -702,6 +705,8 @@ extern "C" int fa_fwd_f16_splitkv(const void* q, const void* k, const void* v, v
   if (head_dim != HD) return FA_ERR_UNSUPPORTED_HEAD_DIM;  // split-KV: head_dim 128 only
   int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
   if (rc != FA_OK) return rc;
+  // fp32 partial rows: the same 32-bit range at 4 bytes per element
+  if ((long long)seq_len * 4 * head_dim > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
   if (num_splits <= 0) num_splits = fa_splitkv_num_splits(batch, heads, seq_len, causal);
   if (num_splits > 64) return FA_ERR_BAD_CONFIG;

@@ -32,7 +32,9 @@ typedef enum {
   FA_OK = 0,
   FA_ERR_NULL_POINTER = 1,        /* q/k/v/o NULL with a non-empty problem */
   FA_ERR_UNSUPPORTED_HEAD_DIM = 2,/* head_dim not 128 (ref :613 HD=128) or 64 */
-  FA_ERR_BAD_SHAPE = 3,           /* negative sizes or int overflow of B*H */
+  FA_ERR_BAD_SHAPE = 3,           /* negative sizes, int overflow of B*H, or
+                                     seq_len*2*head_dim (split-KV: *4) past
+                                     INT_MAX: S <= 8388607 at head_dim 128 */
   FA_ERR_LAUNCH = 4,              /* hipGetLastError() after the launch */
   FA_ERR_BAD_CONFIG = 5,          /* config id out of range / wrong causal */
   FA_ERR_HIP = 6,                 /* other HIP runtime failure */

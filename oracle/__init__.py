@@ -8,6 +8,7 @@ from .fa_oracle import (  # noqa: F401
     ORACLE_LIB,
     attention,
     attention_heads,
+    attention_rows,
     build,
     f16_bits_to_f32,
     gen_inputs,

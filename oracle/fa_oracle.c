@@ -84,9 +84,10 @@ void fa_oracle_gen_inputs(uint16_t* q, uint16_t* k, uint16_t* v, size_t n,
 /* ---- cpu_attention: flash_attention.cu:668-697, one (b,h) head ---- */
 
 /* rows [row_begin, row_end) of one head; rows are independent, so a head can
-   be split over threads without changing any row's operation order */
+   be split over threads without changing any row's operation order.  Row i
+   is written at o + (i - o_row0) * head_dim. */
 static void attention_rows(const uint16_t* q, const uint16_t* k,
-                           const uint16_t* v, uint16_t* o, int seq_len,
+                           const uint16_t* v, uint16_t* o, int o_row0, int seq_len,
                            int head_dim, int causal, int row_begin, int row_end,
                            float* scores, float* qrow) {
   /* :670 scale = 1/sqrtf(head_dim) */
@@ -116,7 +117,7 @@ static void attention_rows(const uint16_t* q, const uint16_t* k,
       float val = 0.0f;
       for (int j = 0; j < end_j; j++)
         val += scores[j] * fa_oracle_f16_to_f32(v[(size_t)j * head_dim + d]);
-      o[(size_t)i * head_dim + d] = fa_oracle_f32_to_f16(val);
+      o[(size_t)(i - o_row0) * head_dim + d] = fa_oracle_f32_to_f16(val);
     }
   }
 }
@@ -142,9 +143,30 @@ void fa_oracle_attention_heads(const uint16_t* q, const uint16_t* k,
       const int c = nchunk - 1 - (int)(it % nchunk);
       const int r1 = (c + 1) * chunk < seq_len ? (c + 1) * chunk : seq_len;
       attention_rows(q + bh * stride, k + bh * stride, v + bh * stride,
-                     o + bh * stride, seq_len, head_dim, causal, c * chunk, r1,
+                     o + bh * stride, 0, seq_len, head_dim, causal, c * chunk, r1,
                      scores, qrow);
     }
+    free(qrow);
+    free(scores);
+  }
+}
+
+/* selected query rows of one head (q, k, v: seq_len x head_dim); o is
+   nrows x head_dim, row r = query row rows[r].  For heads too long for a full
+   pass (the maximum-size GPU tests): each row costs O(seq_len * head_dim). */
+void fa_oracle_attention_rows(const uint16_t* q, const uint16_t* k,
+                              const uint16_t* v, uint16_t* o, int seq_len,
+                              int head_dim, int causal, const int* rows,
+                              int nrows, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+#pragma omp parallel num_threads(n_threads)
+  {
+    float* scores = (float*)malloc((size_t)seq_len * sizeof(float));
+    float* qrow = (float*)malloc((size_t)head_dim * sizeof(float));
+#pragma omp for schedule(dynamic, 1)
+    for (int r = 0; r < nrows; r++)
+      attention_rows(q, k, v, o + (size_t)r * head_dim, rows[r], seq_len, head_dim,
+                     causal, rows[r], rows[r] + 1, scores, qrow);
     free(qrow);
     free(scores);
   }

@@ -60,6 +60,12 @@ void fa_oracle_attention_heads(const uint16_t* q, const uint16_t* k,
 
 /* Reference metric (flash_attention.cu:781-784): max over i of
  * |half2float(a[i]) - half2float(b[i])|. */
+/* selected query rows of one head; o is nrows x head_dim */
+void fa_oracle_attention_rows(const uint16_t* q, const uint16_t* k,
+                              const uint16_t* v, uint16_t* o, int seq_len,
+                              int head_dim, int causal, const int* rows,
+                              int nrows, int n_threads);
+
 float fa_oracle_max_abs_diff(const uint16_t* a, const uint16_t* b, size_t n);
 
 #ifdef __cplusplus

@@ -35,6 +35,8 @@ def load() -> ctypes.CDLL:
         lib.fa_oracle_attention.restype = None
         lib.fa_oracle_attention_heads.argtypes = [vp, vp, vp, vp, i, i, i, i, i, i]
         lib.fa_oracle_attention_heads.restype = None
+        lib.fa_oracle_attention_rows.argtypes = [vp, vp, vp, vp, i, i, i, vp, i, i]
+        lib.fa_oracle_attention_rows.restype = None
         lib.fa_oracle_max_abs_diff.argtypes = [vp, vp, ctypes.c_size_t]
         lib.fa_oracle_max_abs_diff.restype = ctypes.c_float
         lib.fa_oracle_f32_to_f16.argtypes = [ctypes.c_float]
@@ -80,6 +82,21 @@ def attention_heads(q, k, v, bh_begin: int, bh_end: int, causal: bool, threads: 
     threads = threads or max(1, min(os.cpu_count() or 1, 16))
     load().fa_oracle_attention_heads(_p(q), _p(k), _p(v), _p(o), bh_begin, bh_end, s, d,
                                      int(causal), threads)
+    return o
+
+
+def attention_rows(q, k, v, rows, causal: bool, threads: int = 0) -> np.ndarray:
+    """cpu_attention for the query rows `rows` of ONE head (q, k, v: [S, D]
+    uint16 fp16 bits); returns [len(rows), D].  Each row costs O(S * D), so
+    heads far too long for a full pass can be checked by sampling."""
+    s, d = q.shape
+    q, k, v = (np.ascontiguousarray(x, dtype=np.uint16) for x in (q, k, v))
+    r = np.ascontiguousarray(rows, dtype=np.int32)
+    assert r.ndim == 1 and r.size > 0 and r.min() >= 0 and r.max() < s
+    o = np.empty((r.size, d), np.uint16)
+    threads = threads or max(1, min(os.cpu_count() or 1, 16))
+    load().fa_oracle_attention_rows(_p(q), _p(k), _p(v), _p(o), s, d, int(causal), _p(r), r.size,
+                                    threads)
     return o
 
 

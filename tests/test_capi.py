@@ -126,6 +126,10 @@ def test_argument_errors_without_gpu():
     assert _null_call(lib, b=-1) == fa.FA_ERR_BAD_SHAPE
     assert _null_call(lib, s=-5) == fa.FA_ERR_BAD_SHAPE
     assert _null_call(lib) == fa.FA_ERR_NULL_POINTER
+    # a head's byte range must fit the 32-bit buffer resource
+    assert _null_call(lib, s=(1 << 23) - 1) == fa.FA_ERR_NULL_POINTER
+    assert _null_call(lib, s=1 << 23) == fa.FA_ERR_BAD_SHAPE
+    assert _null_call(lib, s=1 << 23, head_dim=64) == fa.FA_ERR_NULL_POINTER
     assert _null_call(lib, b=0) == fa.FA_OK  # empty problem: nothing to launch
     assert _null_call(lib, s=0) == fa.FA_OK
     assert _null_call(lib, b=1 << 16, h=1 << 16) == fa.FA_ERR_BAD_SHAPE
@@ -140,6 +144,9 @@ def test_argument_errors_without_gpu():
         fa.FA_ERR_WORKSPACE
     assert lib.fa_fwd_f16_splitkv(q, q, q, q, 1, 1, 64, 128, 0, 65, q, q, None) == \
         fa.FA_ERR_BAD_CONFIG
+    # fp32 partial rows: half the main path's sequence range
+    assert lib.fa_fwd_f16_splitkv(q, q, q, q, 1, 1, 1 << 22, 128, 0, 2, q, q, None) == \
+        fa.FA_ERR_BAD_SHAPE
 
 
 def test_status_strings():

@@ -5,6 +5,9 @@ take minutes: sampled heads vs the oracle, and size-independent properties.
   of whole heads (first, last, a middle one, plus heads spread over the batch)
   is checked against the oracle at the 1e-3 gate.
 * seq=16384 causal / seq=8192 non-causal (configs 3, 4): sampled heads.
+* maximum sizes: single heads of 64k, 128k and 1M tokens (the kernels take
+  S <= 8388607 at head_dim 128), sampled query rows (block edges, the middle,
+  the last row, random rows) against the oracle's row-sampled entry.
 * properties: V = 1 -> O = 1; causal row 0 -> O[0] = V[0]; a batch split into
   shards gives bit-identical results to the unsharded launch (what bench.py's
   multi-GPU sharding relies on); output is deterministic across launches.
@@ -54,6 +57,30 @@ def _check_sampled(b, h, s, causal, heads, seed=1):
         worst = max(worst, d)
         assert d <= TOL, f"head {flat} (b={bi}, h={hi}): max_diff={d}"
     return worst
+
+
+def _sample_rows(s, n=24, seed=0):
+    rng = np.random.default_rng(seed)
+    edges = [0, 1, 63, 64, 255, 256, s // 2, s - 257, s - 256, s - 64, s - 2, s - 1]
+    return sorted(set(edges) | set(rng.integers(0, s, n).tolist()))
+
+
+@pytest.mark.parametrize("s,h,causal,head_dim", [(65536, 2, True, 128), (65536, 2, False, 128),
+                                                 (131072, 1, False, 128), (131072, 1, True, 128),
+                                                 (1 << 20, 1, True, 128), (65536, 1, True, 64)])
+def test_max_sequence_sampled_rows(s, h, causal, head_dim):
+    fa = _fa()
+    shape = (1, h, s, head_dim)
+    q, k, v = _rand(shape, 21), _rand(shape, 22), _rand(shape, 23)
+    o = fa.flash_attention_fwd(q, k, v, causal=causal)
+    torch.cuda.synchronize()
+    rows = _sample_rows(s)
+    for hi in range(h):
+        qs, ks, vs = (_bits(x[0, hi]) for x in (q, k, v))
+        ref = oracle.attention_rows(qs, ks, vs, rows, causal)
+        got = _bits(o[0, hi])[rows]
+        d = oracle.max_abs_diff(got, ref)
+        assert d <= TOL, f"S={s} head {hi}: max_diff={d}"
 
 
 def test_config5_full_size_sampled_heads():

@@ -134,6 +134,16 @@ def test_heads_subset_matches_full():
     assert not part.reshape(6, -1)[:2].any()
 
 
+@pytest.mark.parametrize("causal", [False, True])
+def test_rows_subset_matches_full(causal):
+    # the row-sampled entry (maximum-size GPU tests) is the same per-row code
+    q, k, v = oracle.gen_inputs(1, 1, 300, 128, 5)
+    full = oracle.attention(q, k, v, causal)[0, 0]
+    rows = [0, 1, 63, 64, 150, 298, 299, 7]
+    got = oracle.attention_rows(q[0, 0], k[0, 0], v[0, 0], rows, causal)
+    np.testing.assert_array_equal(got, full[rows])
+
+
 @pytest.mark.parametrize("name", ["attn_h2_s64_causal", "attn_h2_s64_noncausal",
                                   "attn_h2_s256_causal", "attn_h2_s256_noncausal"])
 def test_golden_fixtures(name):
