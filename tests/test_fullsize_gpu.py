@@ -83,6 +83,15 @@ def test_max_sequence_sampled_rows(s, h, causal, head_dim):
         assert d <= TOL, f"S={s} head {hi}: max_diff={d}"
 
 
+@pytest.mark.parametrize("b,h,s,causal", [(2048, 32, 33, True), (512, 64, 200, False),
+                                           (512, 64, 200, True)])
+def test_many_heads_sampled(b, h, s, causal):
+    # 32-65k heads of a ragged short sequence: grid / item-index arithmetic
+    # at its largest (S=33: 4-wave loop, S=200: persistent tier)
+    n = b * h
+    _check_sampled(b, h, s, causal, [0, 1, h, n // 2 + 3, n - h, n - 2, n - 1])
+
+
 def test_config5_full_size_sampled_heads():
     b, h = 64, 32
     n = b * h
