@@ -34,6 +34,17 @@ def test_op_rejects_cpu_tensors():
         op(q, q, q, False)
 
 
+def test_op_is_forward_only():
+    # no backward formula: refuse loudly instead of zero gradients
+    op = _op()
+    q = torch.empty((1, 2, 64, 128), dtype=torch.float16, device="meta", requires_grad=True)
+    with pytest.raises(RuntimeError, match="forward-only"):
+        op(q, q, q, True)
+    with torch.no_grad():
+        assert op(q, q, q, True).shape == q.shape
+    assert op(q.detach(), q.detach(), q.detach(), False).shape == q.shape
+
+
 def _rand(shape, seed):
     g = torch.Generator(device="cuda")
     g.manual_seed(seed)
