@@ -1318,7 +1318,8 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
 // before the register path would write it), no staging registers.
 // FA_PRIO_MODE (experiment): 0 = s_setprio 1 around every MFMA phase,
 // 1 = none, 2 = static: the younger half (waves 4-7) at priority 1 for the
-// whole loop (guide T5 static form)
+// whole loop (guide T5 static form), 3 = s_setprio 1 around every softmax
+// phase instead (the VALU side first)
 #ifndef FA_PRIO_MODE
 #define FA_PRIO_MODE 0
 #endif
@@ -1465,7 +1466,9 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     if (k < n && active(k)) {
       const int kv0 = kv_lo + k * BN;
       const bool need_mask = (kv0 + BN > kv_hi) || (CAUSAL && kv0 + BN - 1 > qw);
+      if constexpr (PRIO && FA_PRIO_MODE == 3) __builtin_amdgcn_s_setprio(1);
       pol.template softmax<CAUSAL>(kv0, kv_hi, qw, c, need_mask);
+      if constexpr (PRIO && FA_PRIO_MODE == 3) __builtin_amdgcn_s_setprio(0);
     }
   };
 
@@ -1615,6 +1618,11 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
 // that leave CUs idle even at 128 rows (B=1 H=32 S=512: 128 KV-pair
 // workgroups on 256 CUs).  One staging set (loads one half-step ahead): two
 // sets of the double-width stage would not fit the 256 VGPRs.
+// KV-pair / KV-quad priority (A/B knob): 1 = s_setprio 1 around every MFMA
+// half-step (default), 0 = none, 2 = around every softmax half-step instead
+#ifndef FA_KVPAIR_PRIO
+#define FA_KVPAIR_PRIO 1
+#endif
 template <class Pol, bool CAUSAL, int SUB = 1>
 __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int qb, char* smem) {
   static_assert(SUB == 1 || SUB == 2, "key split 2 (KV-pair) or 4 (KV-quad)");
@@ -1784,10 +1792,10 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   for (int m = 0; m < P; ++m) {
     const int h = 2 * m + grp;
     FA_KSTAMP(sa);
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (FA_KVPAIR_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     pol.mfma_block(kbuf(h) + sub * TILE_BYTES, vbuf(h - 2) + sub * TILE_BYTES, active(h - 2),
                    active(h));
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (FA_KVPAIR_PRIO == 1) __builtin_amdgcn_s_setprio(0);
     FA_KSTAMP(sb);
 #ifdef FA_STAMPS
     st_acc[0] += sb - sa;
@@ -1797,7 +1805,9 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
     if (active(h)) {
       const int kv0 = (SUB * h + sub) * BN;
       const bool need_mask = (kv0 + BN > kv_hi) || (CAUSAL && kv0 + BN - 1 > qw);
+      if constexpr (FA_KVPAIR_PRIO == 2) __builtin_amdgcn_s_setprio(1);
       pol.template softmax<CAUSAL>(kv0, kv_hi, qw, c, need_mask);
+      if constexpr (FA_KVPAIR_PRIO == 2) __builtin_amdgcn_s_setprio(0);
     }
     FA_KSTAMP(sb);
 #ifdef FA_STAMPS
