@@ -1056,10 +1056,11 @@ struct M16 {
   // g2 -> 16e+8..15, g3 -> 16(e+1)+8..15.  Half the store instructions
   // (dwordx4 instead of dwordx2) at the same bytes; the store tail is
   // issue-bound (guide T21).
+  template <int B0 = 0, int B1 = QB>  // row blocks [B0, B1) (KV-pair symmetric merge: one each)
   __device__ __forceinline__ void store_o(__amdgpu_buffer_rsrc_t ro, int qw) {
     if constexpr (kAsm) mfma_pad_o();
 #pragma unroll
-    for (int b = 0; b < QB; ++b) {
+    for (int b = B0; b < B1; ++b) {
       const float lt = row_sum(b);  // already the full row sum (MFMA over all keys)
       const float inv = lt > 0.f ? 1.0f / lt : 0.f;
       const int rowb = (qw + 16 * b + r16) * ROW;
@@ -1130,6 +1131,43 @@ struct M16 {
 #endif
       m_ref[b] = M;
     }
+  }
+  // Symmetric KV-pair merge: group A finalizes row block 0 and parks block 1,
+  // group B the reverse.  Region per parked block: NE f32x4 of O, then one
+  // float2 {m, l} per lane.  The combine keeps group A's term first in both
+  // groups, so the result is bit-identical to merge_partial's.
+  static constexpr int HALF_MERGE_BYTES = NE * 64 * 16 + 64 * 8;
+  template <int b>
+  __device__ __forceinline__ void put_block(char* region) const {
+    f32x4* d = reinterpret_cast<f32x4*>(region);
+#pragma unroll
+    for (int e = 0; e < NE; ++e) d[e * 64 + lane] = acc[b][e];
+    reinterpret_cast<float2*>(region + NE * 64 * 16)[lane] = make_float2(m_ref[b], row_sum(b));
+  }
+  template <int b, bool OWN_IS_A>
+  __device__ __forceinline__ void merge_block(const char* region) {
+    const f32x4* d = reinterpret_cast<const f32x4*>(region);
+    const float2 ml = reinterpret_cast<const float2*>(region + NE * 64 * 16)[lane];
+    const float l_own = row_sum(b);
+    const float la = OWN_IS_A ? l_own : ml.y, lb = OWN_IS_A ? ml.y : l_own;
+    const float ma = la > 0.f ? (OWN_IS_A ? m_ref[b] : ml.x) : ninf();
+    const float mb = lb > 0.f ? (OWN_IS_A ? ml.x : m_ref[b]) : ninf();
+    float M = fmaxf(ma, mb);
+    M = M == ninf() ? 0.f : M;
+    const float wa = __builtin_amdgcn_exp2f(ma - M), wb = __builtin_amdgcn_exp2f(mb - M);
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const f32x4 oa = OWN_IS_A ? acc[b][e] : d[e * 64 + lane];
+      const f32x4 ob = OWN_IS_A ? d[e * 64 + lane] : acc[b][e];
+      acc[b][e] = oa * wa + ob * wb;
+    }
+    const float l = la * wa + lb * wb;
+#ifdef FA_ROWSUM_VALU
+    lacc[b] = f32x4{g == 0 ? l : 0.f, 0.f, 0.f, 0.f};
+#else
+    lacc[b] = f32x4{l, l, l, l};
+#endif
+    m_ref[b] = M;
   }
   // m in the reference's units (scaled score, natural log): m_ref * ln 2
   __device__ __forceinline__ void store_partial(__amdgpu_buffer_rsrc_t rpo, float* pml, int qw,
@@ -1618,6 +1656,14 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
 // that leave CUs idle even at 128 rows (B=1 H=32 S=512: 128 KV-pair
 // workgroups on 256 CUs).  One staging set (loads one half-step ahead): two
 // sets of the double-width stage would not fit the 256 VGPRs.
+// KV-pair merge: 1 = symmetric (each group parks one 16-row block and
+// finalizes and stores the other, so all eight waves share the merge and the
+// O stores; bit-identical, level to +1.4 % on the KV-pair shapes,
+// profiles/r02_ab_kvpair_sym_merge.jsonl), 0 = group A merges both blocks
+// and stores all 128 rows (round 1)
+#ifndef FA_KVPAIR_SYM_MERGE
+#define FA_KVPAIR_SYM_MERGE 1
+#endif
 // KV-pair / KV-quad priority (A/B knob): 1 = s_setprio 1 around every MFMA
 // half-step (default), 0 = none, 2 = around every softmax half-step instead
 #ifndef FA_KVPAIR_PRIO
@@ -1825,6 +1871,27 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   // merge: group B parks its partial state, group A combines and stores
   // (FA_DIAG_NO_MERGE: diagnostic timing build only, group A stores its half
   // unmerged -- the merge costs 2-7 % at B=1 H=32 S=512-2048)
+#if FA_KVPAIR_SYM_MERGE && !defined(FA_DIAG_NO_MERGE)
+  if constexpr (SUB == 1) {
+    // symmetric: each group parks one row block and finalizes the other, so
+    // the merge and the O stores are split over all eight waves
+    static_assert(2 * RW * Pol::HALF_MERGE_BYTES <= kKvpairLdsBytes, "half-merge region fits");
+    if (grp == 0)
+      pol.template put_block<1>(smem + rw * Pol::HALF_MERGE_BYTES);
+    else
+      pol.template put_block<0>(smem + (RW + rw) * Pol::HALF_MERGE_BYTES);
+    __syncthreads();
+    const auto ro = make_rsrc(p.o + head_off, S * ROW_BYTES);
+    if (grp == 0) {
+      pol.template merge_block<0, true>(smem + (RW + rw) * Pol::HALF_MERGE_BYTES);
+      pol.template store_o<0, 1>(ro, qw);
+    } else {
+      pol.template merge_block<1, false>(smem + rw * Pol::HALF_MERGE_BYTES);
+      pol.template store_o<1, 2>(ro, qw);
+    }
+    return;
+  }
+#endif
 #ifndef FA_DIAG_NO_MERGE
   // partial j >= 1 of row wave rw parks in slot (j - 1) RW + rw
   if (pidx > 0) pol.put_partial(smem + ((pidx - 1) * RW + rw) * Pol::MERGE_BYTES);
