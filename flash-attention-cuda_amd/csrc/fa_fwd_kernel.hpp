@@ -1293,6 +1293,9 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
     char* kb_next = smem + (BUF ^ 1) * 2 * TILE_BYTES;
     const int kv0 = kv_lo + j * BN;
     FA_TSTAMP(sa);
+#ifdef FA_DIAG_W4_NO_STAGE  // timing-only bound (wrong results): no in-loop K/V staging at 64 rows/wave
+    if constexpr (RW != 64)
+#endif
     issue_loads(kv0 + BN);  // past kv_hi: zero bytes, no memory traffic
     FA_TSTAMP(sb);
     // wave-uniform: does any key of this tile lie at/below some row of this wave?
@@ -1301,6 +1304,9 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
       pol.template tile<CAUSAL>(kb, kb + TILE_BYTES, kv0, kv_hi, qw, c, need_mask);
     }
     FA_TSTAMP(sc);
+#ifdef FA_DIAG_W4_NO_STAGE
+    if constexpr (RW != 64)
+#endif
     write_lds(kb_next);
     FA_TSTAMP(sd);
     __syncthreads();
