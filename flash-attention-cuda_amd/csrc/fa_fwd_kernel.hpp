@@ -1056,7 +1056,8 @@ struct M16 {
   // g2 -> 16e+8..15, g3 -> 16(e+1)+8..15.  Half the store instructions
   // (dwordx4 instead of dwordx2) at the same bytes; the store tail is
   // issue-bound (guide T21).
-  template <int B0 = 0, int B1 = QB>  // row blocks [B0, B1) (KV-pair symmetric merge: one each)
+  // row blocks [B0, B1), d-block pairs [EP0, EP1) (symmetric merges store a part each)
+  template <int B0 = 0, int B1 = QB, int EP0 = 0, int EP1 = NE / 2>
   __device__ __forceinline__ void store_o(__amdgpu_buffer_rsrc_t ro, int qw) {
     if constexpr (kAsm) mfma_pad_o();
 #pragma unroll
@@ -1075,7 +1076,7 @@ struct M16 {
 #else
       const int dlane = 16 * (g & 1) + 8 * (g >> 1);
 #pragma unroll
-      for (int ep = 0; ep < NE / 2; ++ep) {
+      for (int ep = EP0; ep < EP1; ++ep) {
         tx4 wx, wy;
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
@@ -1094,6 +1095,24 @@ struct M16 {
       }
 #endif
     }
+  }
+  // a*wa + b*wb with the contraction fixed (fma(a, wa, b*wb)): left to the
+  // compiler, which product it fuses depends on which operand arrives from
+  // LDS, so two merge paths of the same arithmetic could round differently
+  static __device__ __forceinline__ float mix(float a, float wa, float b, float wb) {
+#ifdef FA_DIAG_FREE_CONTRACT  // A/B only: the compiler picks the contraction
+    return a * wa + b * wb;
+#else
+    return __builtin_fmaf(a, wa, b * wb);
+#endif
+  }
+  static __device__ __forceinline__ f32x4 mix(f32x4 a, float wa, f32x4 b, float wb) {
+#ifdef FA_DIAG_FREE_CONTRACT
+    return a * wa + b * wb;
+#else
+    return f32x4{mix(a[0], wa, b[0], wb), mix(a[1], wa, b[1], wb), mix(a[2], wa, b[2], wb),
+                 mix(a[3], wa, b[3], wb)};
+#endif
   }
   // KV-pair merge (attention_kvpair): the partner wave's state goes through LDS
   // lane-linearly (both waves hold the same query rows in the same lanes).
@@ -1122,8 +1141,8 @@ struct M16 {
       M = M == ninf() ? 0.f : M;
       const float wa = __builtin_amdgcn_exp2f(ma - M), wb = __builtin_amdgcn_exp2f(mb - M);
 #pragma unroll
-      for (int e = 0; e < NE; ++e) acc[b][e] = acc[b][e] * wa + d[(b * NE + e) * 64 + lane] * wb;
-      const float l = la * wa + lb * wb;
+      for (int e = 0; e < NE; ++e) acc[b][e] = mix(acc[b][e], wa, d[(b * NE + e) * 64 + lane], wb);
+      const float l = mix(la, wa, lb, wb);
 #ifdef FA_ROWSUM_VALU
       lacc[b] = f32x4{g == 0 ? l : 0.f, 0.f, 0.f, 0.f};  // row_sum() adds the 4 lanes of a row
 #else
@@ -1159,15 +1178,94 @@ struct M16 {
     for (int e = 0; e < NE; ++e) {
       const f32x4 oa = OWN_IS_A ? acc[b][e] : d[e * 64 + lane];
       const f32x4 ob = OWN_IS_A ? d[e * 64 + lane] : acc[b][e];
-      acc[b][e] = oa * wa + ob * wb;
+      acc[b][e] = mix(oa, wa, ob, wb);
     }
-    const float l = la * wa + lb * wb;
+    const float l = mix(la, wa, lb, wb);
 #ifdef FA_ROWSUM_VALU
     lacc[b] = f32x4{g == 0 ? l : 0.f, 0.f, 0.f, 0.f};
 #else
     lacc[b] = f32x4{l, l, l, l};
 #endif
     m_ref[b] = M;
+  }
+  // Symmetric KV-quad merge: the four partials of a row set each finalize
+  // one quarter -- partial P takes row block P & 1 and d-half P >> 1 -- and
+  // park the three quarters the others finalize (slot (Q - P + 3) & 3 of
+  // their region) plus {m_0, l_0, m_1, l_1}.  Each finalizer replays the
+  // sequential merge of the single-finalizer path (partial 0, then 1, 2, 3;
+  // the accumulated state is always the A side), so the result is
+  // bit-identical to it.
+  static constexpr int QE = NE / 2;  // d-blocks per quarter
+  static constexpr int QUARTER_BYTES = QE * 64 * 16;
+  static constexpr int QUAD_MERGE_BYTES = 3 * QUARTER_BYTES + 64 * 16;
+  __device__ __forceinline__ void put_quarters(char* region, int P) const {
+#pragma unroll
+    for (int Q = 0; Q < 4; ++Q) {
+      if (Q == P) continue;
+      f32x4* d = reinterpret_cast<f32x4*>(region + ((Q - P + 3) & 3) * QUARTER_BYTES);
+#pragma unroll
+      for (int e = 0; e < QE; ++e) d[e * 64 + lane] = acc[Q & 1][(Q >> 1) * QE + e];
+    }
+    reinterpret_cast<f32x4*>(region + 3 * QUARTER_BYTES)[lane] =
+        f32x4{m_ref[0], row_sum(0), m_ref[1], row_sum(1)};
+  }
+  // regions: partial j's region at regions + j * stride
+  template <int P>
+  __device__ __forceinline__ void merge_quarter(const char* regions, int stride) {
+    constexpr int b = P & 1, e0 = (P >> 1) * QE;
+    auto part = [&](int j) { return regions + j * stride; };
+    auto slot = [&](int j) {  // partial j's copy of quarter P
+      return reinterpret_cast<const f32x4*>(part(j) + ((P - j + 3) & 3) * QUARTER_BYTES);
+    };
+    auto ml_of = [&](int j) { return reinterpret_cast<const f32x4*>(part(j) + 3 * QUARTER_BYTES)[lane]; };
+    f32x4 o[QE];
+    float m, l;
+    if constexpr (P == 0) {
+#pragma unroll
+      for (int e = 0; e < QE; ++e) o[e] = acc[b][e0 + e];
+      m = m_ref[b];
+      l = row_sum(b);
+    } else {
+      const f32x4 ml = ml_of(0);
+#pragma unroll
+      for (int e = 0; e < QE; ++e) o[e] = slot(0)[e * 64 + lane];
+      m = ml[2 * b];
+      l = ml[2 * b + 1];
+    }
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      float mj, lj;
+      f32x4 oj[QE];
+      if (j == P) {
+#pragma unroll
+        for (int e = 0; e < QE; ++e) oj[e] = acc[b][e0 + e];
+        mj = m_ref[b];
+        lj = row_sum(b);
+      } else {
+        const f32x4 ml = ml_of(j);
+#pragma unroll
+        for (int e = 0; e < QE; ++e) oj[e] = slot(j)[e * 64 + lane];
+        mj = ml[2 * b];
+        lj = ml[2 * b + 1];
+      }
+      const float ma = l > 0.f ? m : ninf();
+      const float mb = lj > 0.f ? mj : ninf();
+      float M = fmaxf(ma, mb);
+      M = M == ninf() ? 0.f : M;
+      const float wa = __builtin_amdgcn_exp2f(ma - M), wb = __builtin_amdgcn_exp2f(mb - M);
+#pragma unroll
+      for (int e = 0; e < QE; ++e) o[e] = mix(o[e], wa, oj[e], wb);
+      l = mix(l, wa, lj, wb);
+      m = M;
+    }
+#pragma unroll
+    for (int e = 0; e < QE; ++e) acc[b][e0 + e] = o[e];
+#ifdef FA_ROWSUM_VALU
+    lacc[b] = f32x4{g == 0 ? l : 0.f, 0.f, 0.f, 0.f};
+#else
+    lacc[b] = f32x4{l, l, l, l};
+#endif
+    m_ref[b] = m;
   }
   // m in the reference's units (scaled score, natural log): m_ref * ln 2
   __device__ __forceinline__ void store_partial(__amdgpu_buffer_rsrc_t rpo, float* pml, int qw,
@@ -1670,6 +1768,11 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
 #ifndef FA_KVPAIR_SYM_MERGE
 #define FA_KVPAIR_SYM_MERGE 1
 #endif
+// KV-quad merge (A/B knob): 1 = symmetric (each of the four partials of a
+// row set finalizes and stores a quarter), 0 = partial 0 merges all
+#ifndef FA_KVQUAD_SYM_MERGE
+#define FA_KVQUAD_SYM_MERGE 1
+#endif
 // KV-pair / KV-quad priority (A/B knob): 1 = s_setprio 1 around every MFMA
 // half-step (default), 0 = none, 2 = around every softmax half-step instead
 #ifndef FA_KVPAIR_PRIO
@@ -1877,6 +1980,32 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   // merge: group B parks its partial state, group A combines and stores
   // (FA_DIAG_NO_MERGE: diagnostic timing build only, group A stores its half
   // unmerged -- the merge costs 2-7 % at B=1 H=32 S=512-2048)
+#if FA_KVQUAD_SYM_MERGE && !defined(FA_DIAG_NO_MERGE)
+  if constexpr (SUB == 2) {
+    // symmetric: each of a row set's four partials finalizes one quarter
+    static_assert(NP * RW * Pol::QUAD_MERGE_BYTES <= kKvquadLdsBytes, "quarter-merge region fits");
+    const int stride = RW * Pol::QUAD_MERGE_BYTES;
+    char* regions = smem + rw * Pol::QUAD_MERGE_BYTES;  // partial j at regions + j * stride
+    pol.put_quarters(regions + pidx * stride, pidx);
+    __syncthreads();
+    const auto ro = make_rsrc(p.o + head_off, S * ROW_BYTES);
+    constexpr int H = Pol::QE / 2;  // d-block pairs per quarter
+    if (pidx == 0) {
+      pol.template merge_quarter<0>(regions, stride);
+      pol.template store_o<0, 1, 0, H>(ro, qw);
+    } else if (pidx == 1) {
+      pol.template merge_quarter<1>(regions, stride);
+      pol.template store_o<1, 2, 0, H>(ro, qw);
+    } else if (pidx == 2) {
+      pol.template merge_quarter<2>(regions, stride);
+      pol.template store_o<0, 1, H, 2 * H>(ro, qw);
+    } else {
+      pol.template merge_quarter<3>(regions, stride);
+      pol.template store_o<1, 2, H, 2 * H>(ro, qw);
+    }
+    return;
+  }
+#endif
 #if FA_KVPAIR_SYM_MERGE && !defined(FA_DIAG_NO_MERGE)
   if constexpr (SUB == 1) {
     // symmetric: each group parks one row block and finalizes the other, so

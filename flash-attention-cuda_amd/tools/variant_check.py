@@ -19,7 +19,7 @@ for v in ("", var):
     fa.LIB_PATH = os.path.join(HERE, "lib", "libfa_mi355x%s.so" % ("_" + v if v else ""))
     libs[v] = fa.load_library()
 SHAPES = [(1, 32, 4096), (2, 3, 1000), (1, 12, 8192), (1, 48, 2048), (4, 8, 4096), (1, 2, 16384),
-          (1, 32, 1024), (1, 16, 2048), (1, 24, 1536),
+          (1, 32, 1024), (1, 16, 2048), (1, 24, 1536), (1, 32, 512), (1, 8, 2048),
           (8, 32, 1280), (3, 5, 3333)]
 g = torch.Generator(device="cuda")
 g.manual_seed(11)
