@@ -215,6 +215,17 @@ __global__ __launch_bounds__(WAVES * 64, QB == 4 ? 1 : 2) void fa_fwd_f16_persis
 #endif
   const bool pairs =
       FA_CAUSAL_PAIRS && CAUSAL && items.affine && (p.nqb & 1) == 0 && p.band == 1;
+  // Which block of a pair runs first.  Light first (p, then nqb-1-p): CU p
+  // starts its heavy block at key tile 0 when its light one ends, so the
+  // XCD's CUs read K/V inside a window of ~4*32 key tiles that L2 holds if
+  // it fits (nqb <= 32, S <= 8192: 64 tiles x 32 KB = 2 MB at S=8192, HBM
+  // traffic 1.33 -> 1.26x); heavy first otherwise (S=16384: 1.32x vs 1.49x
+  // light first; profiles/r02_pair_light_first.jsonl).  FA_PAIR_LIGHT_FIRST
+  // forces 0 (heavy) or 1 (light).
+#ifndef FA_PAIR_LIGHT_FIRST
+#define FA_PAIR_LIGHT_FIRST -1
+#endif
+  const int light_first = FA_PAIR_LIGHT_FIRST >= 0 ? FA_PAIR_LIGHT_FIRST : (p.nqb <= 32 ? 1 : 0);
   const int npairs = items.hx * (p.nqb >> 1);
   const int rounds = pairs ? 2 * ((npairs + C - 1) / C) : split_tail ? full : (L + C - 1) / C;
   for (int r = 0; r < rounds; ++r) {
@@ -224,7 +235,7 @@ __global__ __launch_bounds__(WAVES * 64, QB == 4 ? 1 : 2) void fa_fwd_f16_persis
       if (pairs) {
         const int half = p.nqb >> 1, lh = pos / half, pp = pos - lh * half;
         bh = x + 8 * lh;
-        qb = (r & 1) ? pp : p.nqb - 1 - pp;
+        qb = ((r & 1) != light_first) ? pp : p.nqb - 1 - pp;
       } else {
         item_of(pos, bh, qb);
       }
