@@ -55,7 +55,8 @@ constexpr int HD = 128;            // head_dim (the reference hard-codes 128, :6
 constexpr int ROW_BYTES = HD * 2;  // one K/V/Q row in bytes
 constexpr float RESCALE_LOG2 = 8.0f;
 // attention_kvpair: 4 tile buffers (64 KB) or the merge region (4 x 17 KB at head_dim 128)
-constexpr int kKvpairLdsBytes = 4 * (2 * 8 + 1) * 64 * 16;
+constexpr int kKvpairLdsBytes =
+    4 * 64 * 256 + 4 * 8 * 64 * 16;  // 4 tile buffers + Q share (4 row sets x 8 KB); >= merge
 // KV-quad: four double-width (128-key) stage buffers
 constexpr int kKvquadLdsBytes = 4 * 2 * 64 * 256;
 
@@ -539,6 +540,42 @@ struct M16 {
       for (int t = 0; t < NTQ; ++t)
 #pragma unroll
         for (int j = 0; j < 8; ++j) qf[b][t][j] = (T)((float)qf[b][t][j] * c);
+    pin_q();
+  }
+  // Q shared by the NPART partial waves of one row set (KV-quad): partial j
+  // loads and scales only the chunks i = NTQ*b + t with i % NPART == j, parks them
+  // lane-linearly in LDS, and reads the others' after the prologue barrier --
+  // one global read of each Q chunk per workgroup instead of NPART
+  static constexpr int Q_SHARE_BYTES = QB * NTQ * 64 * 16;
+  template <int NPART>
+  __device__ __forceinline__ void issue_q_part(__amdgpu_buffer_rsrc_t rq, int qw, int j) {
+#pragma unroll
+    for (int b = 0; b < QB; ++b)
+#pragma unroll
+      for (int t = 0; t < NTQ; ++t)
+        if ((b * NTQ + t) % NPART == j)
+          qf[b][t] = __builtin_bit_cast(
+              tx8, buf_load16(rq, (qw + 16 * b + r16) * ROW + (4 * t + g) * 16));
+  }
+  template <int NPART>
+  __device__ __forceinline__ void scale_put_q_part(char* region, int j) {
+#pragma unroll
+    for (int b = 0; b < QB; ++b)
+#pragma unroll
+      for (int t = 0; t < NTQ; ++t)
+        if ((b * NTQ + t) % NPART == j) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) qf[b][t][e] = (T)((float)qf[b][t][e] * c);
+          reinterpret_cast<tx8*>(region)[(b * NTQ + t) * 64 + lane] = qf[b][t];
+        }
+  }
+  template <int NPART>
+  __device__ __forceinline__ void get_q_rest(const char* region, int j) {
+#pragma unroll
+    for (int b = 0; b < QB; ++b)
+#pragma unroll
+      for (int t = 0; t < NTQ; ++t)
+        if ((b * NTQ + t) % NPART != j) qf[b][t] = reinterpret_cast<const tx8*>(region)[(b * NTQ + t) * 64 + lane];
     pin_q();
   }
   // materialise the scaled Q here: otherwise hipcc sinks the scaling VALU past
@@ -1768,6 +1805,15 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
 #ifndef FA_KVPAIR_SYM_MERGE
 #define FA_KVPAIR_SYM_MERGE 1
 #endif
+// Short-tier Q: 1 = each Q chunk read once per workgroup and shared through
+// LDS by the row set's partial waves (bit-identical; KV-quad +3.5-12.6 %,
+// profiles/r02_ab_short_q_share.jsonl), 0 = every wave loads its own Q
+#ifndef FA_KVQUAD_SHARE_Q
+#define FA_KVQUAD_SHARE_Q 1
+#endif
+#ifndef FA_KVPAIR_SHARE_Q
+#define FA_KVPAIR_SHARE_Q 1
+#endif
 // KV-quad merge (A/B knob): 1 = symmetric (each of the four partials of a
 // row set finalizes and stores a quarter), 0 = partial 0 merges all
 #ifndef FA_KVQUAD_SYM_MERGE
@@ -1838,7 +1884,19 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
 
   Pol pol;
   pol.init(lane, p.c);
-  pol.issue_q(make_rsrc(Qh, S * ROW_BYTES), qw);
+  // the partials of a row set share one read of its Q through LDS: KV-quad
+  // through the stage-0 V buffer (first written after a later barrier),
+  // KV-pair past the four tile buffers (its stage-0 V buffer is too small)
+  constexpr bool kShareQ = SUB == 2 ? FA_KVQUAD_SHARE_Q : FA_KVPAIR_SHARE_Q;
+  char* qshare = smem + (SUB == 2 ? 2 : 4) * STAGE_BYTES + rw * Pol::Q_SHARE_BYTES;
+  static_assert(!kShareQ || SUB == 1 || RW * Pol::Q_SHARE_BYTES <= STAGE_BYTES,
+                "Q share fits one V buffer");
+  static_assert(!kShareQ || SUB == 2 || 4 * STAGE_BYTES + RW * Pol::Q_SHARE_BYTES <= kKvpairLdsBytes,
+                "Q share fits past the tile buffers");
+  if constexpr (kShareQ)
+    pol.template issue_q_part<NP>(make_rsrc(Qh, S * ROW_BYTES), qw, pidx);
+  else
+    pol.issue_q(make_rsrc(Qh, S * ROW_BYTES), qw);
 
   auto kbuf = [&](int x) { return smem + (x & 1) * STAGE_BYTES; };
   auto vbuf = [&](int x) { return smem + (2 + (x & 1)) * STAGE_BYTES; };
@@ -1900,7 +1958,10 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
       issue_stage(0, Set0{});
     }
     __builtin_amdgcn_sched_barrier(0);  // all prologue loads issued first (attention_tile_loop)
-    pol.scale_q();
+    if constexpr (kShareQ)
+      pol.template scale_put_q_part<NP>(qshare, pidx);
+    else
+      pol.scale_q();
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
       *reinterpret_cast<f16x8*>(kbuf(0) + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = k0[i];
@@ -1908,6 +1969,7 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   // Q and K_0 retired (see attention_tile_loop); the stage loads may stay in flight
   __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * NSET * NCH));
   __syncthreads();
+  if constexpr (kShareQ) pol.template get_q_rest<NP>(qshare, pidx);
 #ifdef FA_STAMPS
   st_acc[7] = __builtin_amdgcn_s_memtime() - t_in;
 #endif

@@ -60,6 +60,9 @@ def test_exports_reference_cpp_signature():
                      out), out
 
 
+KVPAIR_LDS = 4 * 64 * 256 + 4 * 8 * 64 * 16  # tile buffers + shared Q (csrc kKvpairLdsBytes)
+
+
 def test_config_table():
     fa = _fa()
     cfgs = fa.configs()
@@ -68,10 +71,10 @@ def test_config_table():
         assert c.head_dim in (64, 128) and c.dtype in ("float16", "bfloat16")
         assert c.block_n % 32 == 0
         if "_kvpair_" in c.name:
-            # two waves per 32 query rows; LDS = 4 tile buffers or the merge
-            # region (4 waves x (16 O + 1 m/l) x 64 lanes x 16 B), the larger
+            # two waves per 32 query rows; LDS = 4 tile buffers + the shared
+            # Q of 4 row sets (8 KB each), which also covers the merge region
             assert c.block_m == 16 * c.waves
-            assert c.lds_bytes == max(4 * c.block_n * 256, 4 * 17 * 64 * 16)
+            assert c.lds_bytes == KVPAIR_LDS >= 4 * 17 * 64 * 16
             continue
         if "_kvquad_" in c.name:
             # four waves per 32 query rows; four double-width stage buffers
@@ -85,7 +88,7 @@ def test_config_table():
         nbuf = 3 if "_dma_" in c.name else 2
         need = 2 * nbuf * c.block_n * 256
         if "_pingpong_persistent_" in c.name and "_dma_" not in c.name and not c.causal:
-            need = max(need, 4 * 17 * 64 * 16)  # room for the KV-pair tail halves
+            need = max(need, KVPAIR_LDS)  # room for the KV-pair tail halves
         assert c.lds_bytes == need <= 160 * 1024
     # every (waves, bn) non-split config exists for both masks
     nonsplit = {(c.waves, c.block_n, c.causal) for c in cfgs if not c.split_kv}
