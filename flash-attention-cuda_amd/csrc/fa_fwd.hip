@@ -635,7 +635,14 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   const bool persist = causal ? (wg256 >= 384 || (wg256 >= 256 && nqb256 <= 2)) : wg256 >= 160;
   if (persist) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 2);
   if (seq_len <= 256) return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
-  if (wg64 <= 256) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 4);
+  // causal, two rounds of 64-row blocks over long heads (>= 32 blocks per
+  // head): the KV-quad's four-way key split halves the heaviest block's key
+  // loop against the KV-pair (B=1 H=4 S=8192 765 vs 599, H=2 S=16384 808 vs
+  // 623, H=8 S=4096 694 vs 562, H=16 S=2048 544 vs 513; at S=1024 or past
+  // 512 blocks the KV-pair still wins: profiles/r02_pair_vs_quad.jsonl)
+  const long long nqb64 = (seq_len + 63) / 64;
+  if (wg64 <= 256 || (causal && wg64 <= 512 && nqb64 >= 32))
+    return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 4);
   if (wg128 <= 512) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 3);
   return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
 }

@@ -113,6 +113,11 @@ def test_select_config(causal):
     assert "_kvquad_" in cfgs[fa.select_config(1, 8, 2048, causal)].name
     assert "_kvquad_" in cfgs[fa.select_config(1, 32, 512, causal)].name
     assert "_w4_" in cfgs[fa.select_config(1, 32, 256, causal)].name
+    # causal, two rounds of 64-row blocks over long heads: the KV-quad's
+    # four-way key split; non-causal (and S=1024) stay on the KV-pair
+    want = "_kvquad_" if causal else "_kvpair_"
+    for b, h, s in ((1, 4, 8192), (1, 2, 16384), (1, 8, 4096), (1, 16, 2048)):
+        assert want in cfgs[fa.select_config(b, h, s, causal)].name, (b, h, s, causal)
 
 
 def _null_call(lib, head_dim=128, b=1, h=1, s=64, causal=0, ptr=None):
