@@ -55,8 +55,12 @@ constexpr int HD = 128;            // head_dim (the reference hard-codes 128, :6
 constexpr int ROW_BYTES = HD * 2;  // one K/V/Q row in bytes
 constexpr float RESCALE_LOG2 = 8.0f;
 // attention_kvpair: 4 tile buffers (64 KB) or the merge region (4 x 17 KB at head_dim 128)
+#ifndef FA_KVPAIR_SHARE_Q
+#define FA_KVPAIR_SHARE_Q 1
+#endif
 constexpr int kKvpairLdsBytes =
-    4 * 64 * 256 + 4 * 8 * 64 * 16;  // 4 tile buffers + Q share (4 row sets x 8 KB); >= merge
+    FA_KVPAIR_SHARE_Q ? 4 * 64 * 256 + 4 * 8 * 64 * 16  // 4 tile buffers + shared Q (4 x 8 KB)
+                      : 4 * (2 * 8 + 1) * 64 * 16;      // 4 tile buffers or the merge region
 // KV-quad: four double-width (128-key) stage buffers
 constexpr int kKvquadLdsBytes = 4 * 2 * 64 * 256;
 
@@ -1810,9 +1814,6 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
 // profiles/r02_ab_short_q_share.jsonl), 0 = every wave loads its own Q
 #ifndef FA_KVQUAD_SHARE_Q
 #define FA_KVQUAD_SHARE_Q 1
-#endif
-#ifndef FA_KVPAIR_SHARE_Q
-#define FA_KVPAIR_SHARE_Q 1
 #endif
 // KV-quad merge (A/B knob): 1 = symmetric (each of the four partials of a
 // row set finalizes and stores a quarter), 0 = partial 0 merges all
