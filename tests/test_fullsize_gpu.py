@@ -83,6 +83,26 @@ def test_max_sequence_sampled_rows(s, h, causal, head_dim):
         assert d <= TOL, f"S={s} head {hi}: max_diff={d}"
 
 
+@pytest.mark.parametrize("b,h,s", [(1, 4, 8192), (1, 2, 16384), (1, 8, 4096), (2, 8, 2048)])
+def test_long_causal_few_heads_kvquad(b, h, s):
+    # the selector sends these causal launches to the KV-quad (four-way key
+    # split over long heads): sampled rows of every head against the oracle
+    fa = _fa()
+    cfg = fa.configs()[fa.select_config(b, h, s, True)].name
+    assert "_kvquad_" in cfg, cfg
+    shape = (b, h, s, 128)
+    q, k, v = _rand(shape, 31), _rand(shape, 32), _rand(shape, 33)
+    o = fa.flash_attention_fwd(q, k, v, causal=True)
+    torch.cuda.synchronize()
+    rows = _sample_rows(s, n=12)
+    for bi in range(b):
+        for hi in range(h):
+            qs, ks, vs = (_bits(x[bi, hi]) for x in (q, k, v))
+            ref = oracle.attention_rows(qs, ks, vs, rows, True)
+            d = oracle.max_abs_diff(_bits(o[bi, hi])[rows], ref)
+            assert d <= TOL, f"b={bi} h={hi}: max_diff={d}"
+
+
 @pytest.mark.parametrize("b,h,s,causal", [(2048, 32, 33, True), (512, 64, 200, False),
                                            (512, 64, 200, True)])
 def test_many_heads_sampled(b, h, s, causal):
