@@ -187,7 +187,10 @@ def _source_files():
     import glob
 
     out = []
-    for pat in ("csrc/*.hip", "csrc/*.hpp", "csrc/*.cpp", "csrc/*.h", "asm/*.py", "Makefile"):
+    # every file the library is compiled from, generated includes and their
+    # generators included
+    for pat in ("csrc/*.hip", "csrc/*.hpp", "csrc/*.cpp", "csrc/*.h", "csrc/*.inc", "csrc/*.py",
+                "asm/*.py", "Makefile"):
         out += [os.path.relpath(f, PKG) for f in glob.glob(os.path.join(PKG, pat))]
     return sorted(out)
 

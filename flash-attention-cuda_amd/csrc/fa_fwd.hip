@@ -66,30 +66,24 @@ __device__ __forceinline__ void map_block(int id, int nblk, int nqb, int bh_coun
 }
 
 // SCHED: 0 = one-barrier-per-tile loop (any wave count), 1 = 8-wave ping-pong
-// (MFMA phase at s_setprio 1), 2 = ping-pong without the priority raise,
-// 3 = ping-pong with LDS-DMA tile loads into three rotating buffers
-// BF16: Q/K/V/O and the MFMA operands are bf16 (16x16x32 policy only)
-// HDIM: head_dim (64 runs on the 16x16x32 policy only)
-template <int WAVES, int BN, bool CAUSAL, bool SPLIT, bool USE_M16, int SCHED, bool BF16 = false,
-          int HDIM = 128, int QB = 2>
+// (MFMA phase at s_setprio 1), 3 = ping-pong with LDS-DMA tile loads into
+// three rotating buffers
+// BF16: Q/K/V/O and the MFMA operands are bf16
+// HDIM: head_dim (128 or 64)
+template <int WAVES, int BN, bool CAUSAL, bool SPLIT, int SCHED, bool BF16 = false, int HDIM = 128>
 __device__ __forceinline__ void run_tile_loop(const FwdParams& p, int bh, int qb, int split,
                                               char* smem) {
-  static_assert(USE_M16 || (!BF16 && HDIM == 128), "bf16 / head_dim 64 run on the 16x16x32 policy");
-  using Pol = typename std::conditional<
-      USE_M16, M16<BN, typename std::conditional<BF16, __bf16, f16>::type, HDIM, QB>, M32<BN>>::type;
-  if constexpr (SCHED == 1 || SCHED == 2 || SCHED == 3) {
+  using Pol = M16<BN, typename std::conditional<BF16, __bf16, f16>::type, HDIM>;
+  if constexpr (SCHED == 1 || SCHED == 3) {
     static_assert(WAVES == 8, "ping-pong needs two groups of four waves");
-    attention_pingpong<Pol, CAUSAL, SPLIT, SCHED != 2, SCHED == 3>(p, bh, qb, split, smem);
+    attention_pingpong<Pol, CAUSAL, SPLIT, true, SCHED == 3>(p, bh, qb, split, smem);
   } else {
     attention_tile_loop<Pol, WAVES, CAUSAL, SPLIT>(p, bh, qb, split, smem);
   }
 }
 
-// QB = 4: 64 query rows per wave, one wave per SIMD (the whole 512-entry
-// register file per wave)
-template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED, bool BF16 = false,
-          int HDIM = 128, int QB = 2>
-__global__ __launch_bounds__(WAVES * 64, QB == 4 ? 1 : 2) void fa_fwd_f16_kernel(FwdParams p) {
+template <int WAVES, int BN, bool CAUSAL, int SCHED, bool BF16 = false, int HDIM = 128>
+__global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 #ifdef FA_STAMPS
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
@@ -97,7 +91,7 @@ __global__ __launch_bounds__(WAVES * 64, QB == 4 ? 1 : 2) void fa_fwd_f16_kernel
 #endif
   int qb, bh;
   map_block(blockIdx.x, gridDim.x, p.nqb, p.bh, p.band, CAUSAL, qb, bh);
-  run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED, BF16, HDIM, QB>(p, bh, qb, 0, smem);
+  run_tile_loop<WAVES, BN, CAUSAL, false, SCHED, BF16, HDIM>(p, bh, qb, 0, smem);
 #ifdef FA_STAMPS
   if (threadIdx.x == 0 && blockIdx.x < FA_MAX_TIMELINE) {
     unsigned hw, xcc;
@@ -178,9 +172,8 @@ struct XcdItems {
   }
 };
 
-template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED, bool BF16 = false,
-          int HDIM = 128, int QB = 2>
-__global__ __launch_bounds__(WAVES * 64, QB == 4 ? 1 : 2) void fa_fwd_f16_persistent_kernel(
+template <int WAVES, int BN, bool CAUSAL, int SCHED, bool BF16 = false, int HDIM = 128>
+__global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(
     FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int x = blockIdx.x & 7, lcu = blockIdx.x >> 3, C = gridDim.x >> 3;
@@ -190,11 +183,7 @@ __global__ __launch_bounds__(WAVES * 64, QB == 4 ? 1 : 2) void fa_fwd_f16_persis
   // Non-causal tail: items cost the same, so a last round of `tail` <= C/2
   // items would leave C - tail CUs idle (1.5 items per CU: 75 %).  Those
   // items run instead as 2*tail 128-row KV-pair halves on 2*tail CUs.
-#ifdef FA_NO_TAIL_SPLIT
-  constexpr bool kTailSplit = false;
-#else
   constexpr bool kTailSplit = !CAUSAL && SCHED == 1;
-#endif
   const int full = L / C, tail = L - full * C;
   const bool split_tail = kTailSplit && tail > 0 && 2 * tail <= C;
   // Causal pair order: CU lcu runs the two query blocks (nqb-1-p, p) of one
@@ -210,22 +199,14 @@ __global__ __launch_bounds__(WAVES * 64, QB == 4 ? 1 : 2) void fa_fwd_f16_persis
   // band-16 snake co-starts whole heads and fetches less (B=64 S=4096: 1.07x
   // vs 1.41x), so pairs replace only the plain heaviest-first order (band 1,
   // <= 64 heads; profiles/r02_causal_pairs_{ab,traffic}.jsonl).
-#ifndef FA_CAUSAL_PAIRS
-#define FA_CAUSAL_PAIRS 1
-#endif
-  const bool pairs =
-      FA_CAUSAL_PAIRS && CAUSAL && items.affine && (p.nqb & 1) == 0 && p.band == 1;
+  const bool pairs = CAUSAL && items.affine && (p.nqb & 1) == 0 && p.band == 1;
   // Which block of a pair runs first.  Light first (p, then nqb-1-p): CU p
   // starts its heavy block at key tile 0 when its light one ends, so the
   // XCD's CUs read K/V inside a window of ~4*32 key tiles that L2 holds if
   // it fits (nqb <= 32, S <= 8192: 64 tiles x 32 KB = 2 MB at S=8192, HBM
   // traffic 1.33 -> 1.26x); heavy first otherwise (S=16384: 1.32x vs 1.49x
-  // light first; profiles/r02_pair_light_first.jsonl).  FA_PAIR_LIGHT_FIRST
-  // forces 0 (heavy) or 1 (light).
-#ifndef FA_PAIR_LIGHT_FIRST
-#define FA_PAIR_LIGHT_FIRST -1
-#endif
-  const int light_first = FA_PAIR_LIGHT_FIRST >= 0 ? FA_PAIR_LIGHT_FIRST : (p.nqb <= 32 ? 1 : 0);
+  // light first; profiles/r02_pair_light_first.jsonl).
+  const int light_first = p.nqb <= 32 ? 1 : 0;
   const int npairs = items.hx * (p.nqb >> 1);
   const int rounds = pairs ? 2 * ((npairs + C - 1) / C) : split_tail ? full : (L + C - 1) / C;
   for (int r = 0; r < rounds; ++r) {
@@ -243,7 +224,7 @@ __global__ __launch_bounds__(WAVES * 64, QB == 4 ? 1 : 2) void fa_fwd_f16_persis
       const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
       const unsigned long long c_start = __builtin_amdgcn_s_memtime();
 #endif
-      run_tile_loop<WAVES, BN, CAUSAL, false, USE_M16, SCHED, BF16, HDIM, QB>(p, bh, qb, 0, smem);
+      run_tile_loop<WAVES, BN, CAUSAL, false, SCHED, BF16, HDIM>(p, bh, qb, 0, smem);
 #ifdef FA_STAMPS
       const int rec = bh * p.nqb + qb;
       if (threadIdx.x == 0 && rec < FA_MAX_TIMELINE) {
@@ -300,14 +281,14 @@ __global__ __launch_bounds__(512, 2) void fa_fwd_f16_kvpair_kernel(FwdParams p) 
 }
 
 // Split-KV: workgroup id -> (split, item); items ordered as map_block.
-template <int WAVES, int BN, bool CAUSAL, bool USE_M16, int SCHED>
+template <int WAVES, int BN, bool CAUSAL, int SCHED>
 __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_splitkv_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int split = blockIdx.x % p.num_splits;
   const int item = blockIdx.x / p.num_splits;
   int qb, bh;
   map_block(item, gridDim.x / p.num_splits, p.nqb, p.bh, 0, CAUSAL, qb, bh);
-  run_tile_loop<WAVES, BN, CAUSAL, true, USE_M16, SCHED>(p, bh, qb, split, smem);
+  run_tile_loop<WAVES, BN, CAUSAL, true, SCHED>(p, bh, qb, split, smem);
 }
 
 // Log-sum-exp merge of split partials (ref flash_attention_splitk_merge,
@@ -347,114 +328,95 @@ typedef void (*kernel_fn)(FwdParams);
 
 struct Config {
   fa_config_info_t info;
-  int mfma;   // 32 = v_mfma_f32_32x32x16_f16 loop, 16 = v_mfma_f32_16x16x32_f16 loop
-  int sched;  // 0 = one barrier per tile, 1 = 8-wave ping-pong
+  int sched;  // 0 = one barrier per tile, 1 = 8-wave ping-pong, 3 = ping-pong + LDS-DMA tiles
   int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent, 3 = KV-pair,
               // 4 = KV-quad
   kernel_fn fn;
 };
 
-template <int W, int BN_, int C, int SPL, int M, int SCHED, int DT, int HDIM, int QB = 2>
+template <int W, int BN_, int C, int KIND, int SCHED, int DT, int HDIM>
 constexpr kernel_fn pick_kernel() {
-  if constexpr (SPL == 3)
+  if constexpr (KIND == 3)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
-  else if constexpr (SPL == 4)
+  else if constexpr (KIND == 4)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM, 2>;
-
-  else if constexpr (SPL == 1)
-    return fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0), (M == 16), SCHED>;
-  else if constexpr (SPL == 2)
-    return fa_fwd_f16_persistent_kernel<W, BN_, (C != 0), (M == 16), SCHED, DT == 1, HDIM, QB>;
+  else if constexpr (KIND == 1)
+    return fa_fwd_f16_splitkv_kernel<W, BN_, (C != 0), SCHED>;
+  else if constexpr (KIND == 2)
+    return fa_fwd_f16_persistent_kernel<W, BN_, (C != 0), SCHED, DT == 1, HDIM>;
   else
-    return fa_fwd_f16_kernel<W, BN_, (C != 0), (M == 16), SCHED, DT == 1, HDIM, QB>;
+    return fa_fwd_f16_kernel<W, BN_, (C != 0), SCHED, DT == 1, HDIM>;
 }
 
 // KIND: 0 = one workgroup per (head, query block), 1 = split-KV, 2 = persistent
 // DT: 0 = fp16, 1 = bf16 (FA_DTYPE_*)
 // LDS images keep 256-B row slots at head_dim 64 too (fa_fwd_kernel.hpp M16)
-#define FA_CFG_TD(ID, W, BN_, C, KIND, M, SCHED, DT, HDIM, NAME)                           \
+#define FA_CFG_TD(ID, W, BN_, C, KIND, SCHED, DT, HDIM, NAME)                              \
   {{ID, 32 * (W), BN_, W, C, (KIND) == 1,                                                    \
     ((SCHED) == 3 ? 6 * (BN_) * ROW_BYTES                                                   \
      : ((KIND) == 2 && !(C)) ? std::max(4 * (BN_) * ROW_BYTES, kKvpairLdsBytes) /* tail */ \
                    : 4 * (BN_) * ROW_BYTES),                                                \
-    NAME, DT, HDIM}, M, SCHED,                                                              \
-   KIND, pick_kernel<W, BN_, C, KIND, M, SCHED, DT, HDIM>()}
-#define FA_CFG_T(ID, W, BN_, C, KIND, M, SCHED, DT, NAME) \
-  FA_CFG_TD(ID, W, BN_, C, KIND, M, SCHED, DT, 128, NAME)
-#define FA_CFG(ID, W, BN_, C, KIND, M, SCHED, NAME) FA_CFG_T(ID, W, BN_, C, KIND, M, SCHED, 0, NAME)
+    NAME, DT, HDIM}, SCHED,                                                                 \
+   KIND, pick_kernel<W, BN_, C, KIND, SCHED, DT, HDIM>()}
+#define FA_CFG_T(ID, W, BN_, C, KIND, SCHED, DT, NAME) \
+  FA_CFG_TD(ID, W, BN_, C, KIND, SCHED, DT, 128, NAME)
+#define FA_CFG(ID, W, BN_, C, KIND, SCHED, NAME) FA_CFG_T(ID, W, BN_, C, KIND, SCHED, 0, NAME)
 // KV-pair: 8 waves on 128 query rows (two waves per row block, key range split)
 #define FA_CFG_KVPAIR(ID, C, DT, HDIM, NAME)                                           \
-  {{ID, 128, 64, 8, C, 0, kKvpairLdsBytes, NAME, DT, HDIM}, 16, 1, 3,                   \
-   pick_kernel<8, 64, C, 3, 16, 1, DT, HDIM>()}
+  {{ID, 128, 64, 8, C, 0, kKvpairLdsBytes, NAME, DT, HDIM}, 1, 3,                       \
+   pick_kernel<8, 64, C, 3, 1, DT, HDIM>()}
 // KV-quad: 8 waves on 64 query rows (four waves per row block, key range split four ways)
 #define FA_CFG_KVQUAD(ID, C, DT, HDIM, NAME)                                           \
-  {{ID, 64, 64, 8, C, 0, kKvquadLdsBytes, NAME, DT, HDIM}, 16, 1, 4,                    \
-   pick_kernel<8, 64, C, 4, 16, 1, DT, HDIM>()}
+  {{ID, 64, 64, 8, C, 0, kKvquadLdsBytes, NAME, DT, HDIM}, 1, 4,                        \
+   pick_kernel<8, 64, C, 4, 1, DT, HDIM>()}
 
-// 4 waves x 64 query rows (one wave per SIMD, 512 registers each), one
-// barrier per tile: half the LDS bytes per FLOP of the 32-row waves
-#define FA_CFG_W4X64(ID, C, KIND, SCHED, NAME)                                  \
-  {{ID, 256, 64, 4, C, 0, 4 * 64 * ROW_BYTES, NAME, 0, 128}, 16, SCHED, KIND,    \
-   pick_kernel<4, 64, C, KIND, 16, SCHED, 0, 128, 4>()}
-
+// Only tiers the dispatcher picks, explicit entry points (split-KV) and the
+// baselines a test compares against (the per-item ping-pong 2/3: the
+// persistent kernel must reproduce it bit for bit; LDS-DMA 20/21) ship.
 static const Config kConfigs[] = {
-    FA_CFG(0, 4, 64, 0, 0, 32, 0, "bm128_bn64_w4_m32_noncausal"),
-    FA_CFG(1, 4, 64, 1, 0, 32, 0, "bm128_bn64_w4_m32_causal"),
-    FA_CFG(2, 8, 64, 0, 0, 32, 0, "bm256_bn64_w8_m32_noncausal"),
-    FA_CFG(3, 8, 64, 1, 0, 32, 0, "bm256_bn64_w8_m32_causal"),
-    FA_CFG(4, 4, 64, 0, 0, 16, 0, "bm128_bn64_w4_m16_noncausal"),
-    FA_CFG(5, 4, 64, 1, 0, 16, 0, "bm128_bn64_w4_m16_causal"),
-    FA_CFG(6, 8, 64, 0, 0, 16, 0, "bm256_bn64_w8_m16_noncausal"),
-    FA_CFG(7, 8, 64, 1, 0, 16, 0, "bm256_bn64_w8_m16_causal"),
-    FA_CFG(8, 8, 64, 0, 0, 16, 1, "bm256_bn64_w8_m16_pingpong_noncausal"),
-    FA_CFG(9, 8, 64, 1, 0, 16, 1, "bm256_bn64_w8_m16_pingpong_causal"),
-    FA_CFG(10, 8, 64, 0, 0, 32, 1, "bm256_bn64_w8_m32_pingpong_noncausal"),
-    FA_CFG(11, 8, 64, 1, 0, 32, 1, "bm256_bn64_w8_m32_pingpong_causal"),
-    FA_CFG(12, 4, 64, 0, 1, 16, 0, "bm128_bn64_w4_m16_noncausal_splitkv"),
-    FA_CFG(13, 4, 64, 1, 1, 16, 0, "bm128_bn64_w4_m16_causal_splitkv"),
-    FA_CFG(14, 8, 64, 0, 2, 16, 1, "bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
-    FA_CFG(15, 8, 64, 1, 2, 16, 1, "bm256_bn64_w8_m16_pingpong_persistent_causal"),
+    FA_CFG(0, 4, 64, 0, 0, 0, "bm128_bn64_w4_m16_noncausal"),
+    FA_CFG(1, 4, 64, 1, 0, 0, "bm128_bn64_w4_m16_causal"),
+    FA_CFG(2, 8, 64, 0, 0, 1, "bm256_bn64_w8_m16_pingpong_noncausal"),
+    FA_CFG(3, 8, 64, 1, 0, 1, "bm256_bn64_w8_m16_pingpong_causal"),
+    FA_CFG(4, 4, 64, 0, 1, 0, "bm128_bn64_w4_m16_noncausal_splitkv"),
+    FA_CFG(5, 4, 64, 1, 1, 0, "bm128_bn64_w4_m16_causal_splitkv"),
+    FA_CFG(6, 8, 64, 0, 2, 1, "bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
+    FA_CFG(7, 8, 64, 1, 2, 1, "bm256_bn64_w8_m16_pingpong_persistent_causal"),
     // bf16 twins of the dispatched fp16 tiers
-    FA_CFG_T(16, 4, 64, 0, 0, 16, 0, 1, "bf16_bm128_bn64_w4_m16_noncausal"),
-    FA_CFG_T(17, 4, 64, 1, 0, 16, 0, 1, "bf16_bm128_bn64_w4_m16_causal"),
-    FA_CFG_T(18, 8, 64, 0, 2, 16, 1, 1, "bf16_bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
-    FA_CFG_T(19, 8, 64, 1, 2, 16, 1, 1, "bf16_bm256_bn64_w8_m16_pingpong_persistent_causal"),
+    FA_CFG_T(8, 4, 64, 0, 0, 0, 1, "bf16_bm128_bn64_w4_m16_noncausal"),
+    FA_CFG_T(9, 4, 64, 1, 0, 0, 1, "bf16_bm128_bn64_w4_m16_causal"),
+    FA_CFG_T(10, 8, 64, 0, 2, 1, 1, "bf16_bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
+    FA_CFG_T(11, 8, 64, 1, 2, 1, 1, "bf16_bm256_bn64_w8_m16_pingpong_persistent_causal"),
     // head_dim 64 twins (fp16, bf16)
-    FA_CFG_TD(20, 4, 64, 0, 0, 16, 0, 0, 64, "d64_bm128_bn64_w4_m16_noncausal"),
-    FA_CFG_TD(21, 4, 64, 1, 0, 16, 0, 0, 64, "d64_bm128_bn64_w4_m16_causal"),
-    FA_CFG_TD(22, 8, 64, 0, 2, 16, 1, 0, 64, "d64_bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
-    FA_CFG_TD(23, 8, 64, 1, 2, 16, 1, 0, 64, "d64_bm256_bn64_w8_m16_pingpong_persistent_causal"),
-    FA_CFG_TD(24, 4, 64, 0, 0, 16, 0, 1, 64, "bf16_d64_bm128_bn64_w4_m16_noncausal"),
-    FA_CFG_TD(25, 4, 64, 1, 0, 16, 0, 1, 64, "bf16_d64_bm128_bn64_w4_m16_causal"),
-    FA_CFG_TD(26, 8, 64, 0, 2, 16, 1, 1, 64,
-              "bf16_d64_bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
-    FA_CFG_TD(27, 8, 64, 1, 2, 16, 1, 1, 64, "bf16_d64_bm256_bn64_w8_m16_pingpong_persistent_causal"),
+    FA_CFG_TD(12, 4, 64, 0, 0, 0, 0, 64, "d64_bm128_bn64_w4_m16_noncausal"),
+    FA_CFG_TD(13, 4, 64, 1, 0, 0, 0, 64, "d64_bm128_bn64_w4_m16_causal"),
+    FA_CFG_TD(14, 8, 64, 0, 2, 1, 0, 64, "d64_bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
+    FA_CFG_TD(15, 8, 64, 1, 2, 1, 0, 64, "d64_bm256_bn64_w8_m16_pingpong_persistent_causal"),
+    FA_CFG_TD(16, 4, 64, 0, 0, 0, 1, 64, "bf16_d64_bm128_bn64_w4_m16_noncausal"),
+    FA_CFG_TD(17, 4, 64, 1, 0, 0, 1, 64, "bf16_d64_bm128_bn64_w4_m16_causal"),
+    FA_CFG_TD(18, 8, 64, 0, 2, 1, 1, 64, "bf16_d64_bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
+    FA_CFG_TD(19, 8, 64, 1, 2, 1, 1, 64, "bf16_d64_bm256_bn64_w8_m16_pingpong_persistent_causal"),
     // K/V by LDS-DMA into three rotating LDS buffers
-    FA_CFG(28, 8, 64, 0, 2, 16, 3, "bm256_bn64_w8_m16_pingpong_persistent_dma_noncausal"),
-    FA_CFG(29, 8, 64, 1, 2, 16, 3, "bm256_bn64_w8_m16_pingpong_persistent_dma_causal"),
+    FA_CFG(20, 8, 64, 0, 2, 3, "bm256_bn64_w8_m16_pingpong_persistent_dma_noncausal"),
+    FA_CFG(21, 8, 64, 1, 2, 3, "bm256_bn64_w8_m16_pingpong_persistent_dma_causal"),
     // KV-pair (short sequences): the two waves of a SIMD split the keys of 32 query rows
-    FA_CFG_KVPAIR(30, 0, 0, 128, "bm128_bn64_w8_m16_kvpair_noncausal"),
-    FA_CFG_KVPAIR(31, 1, 0, 128, "bm128_bn64_w8_m16_kvpair_causal"),
-    FA_CFG_KVPAIR(32, 0, 1, 128, "bf16_bm128_bn64_w8_m16_kvpair_noncausal"),
-    FA_CFG_KVPAIR(33, 1, 1, 128, "bf16_bm128_bn64_w8_m16_kvpair_causal"),
-    FA_CFG_KVPAIR(34, 0, 0, 64, "d64_bm128_bn64_w8_m16_kvpair_noncausal"),
-    FA_CFG_KVPAIR(35, 1, 0, 64, "d64_bm128_bn64_w8_m16_kvpair_causal"),
-    FA_CFG_KVPAIR(36, 0, 1, 64, "bf16_d64_bm128_bn64_w8_m16_kvpair_noncausal"),
-    FA_CFG_KVPAIR(37, 1, 1, 64, "bf16_d64_bm128_bn64_w8_m16_kvpair_causal"),
+    FA_CFG_KVPAIR(22, 0, 0, 128, "bm128_bn64_w8_m16_kvpair_noncausal"),
+    FA_CFG_KVPAIR(23, 1, 0, 128, "bm128_bn64_w8_m16_kvpair_causal"),
+    FA_CFG_KVPAIR(24, 0, 1, 128, "bf16_bm128_bn64_w8_m16_kvpair_noncausal"),
+    FA_CFG_KVPAIR(25, 1, 1, 128, "bf16_bm128_bn64_w8_m16_kvpair_causal"),
+    FA_CFG_KVPAIR(26, 0, 0, 64, "d64_bm128_bn64_w8_m16_kvpair_noncausal"),
+    FA_CFG_KVPAIR(27, 1, 0, 64, "d64_bm128_bn64_w8_m16_kvpair_causal"),
+    FA_CFG_KVPAIR(28, 0, 1, 64, "bf16_d64_bm128_bn64_w8_m16_kvpair_noncausal"),
+    FA_CFG_KVPAIR(29, 1, 1, 64, "bf16_d64_bm128_bn64_w8_m16_kvpair_causal"),
     // KV-quad (shortest sequences): four waves split the keys of 32 query rows
-    FA_CFG_KVQUAD(38, 0, 0, 128, "bm64_bn64_w8_m16_kvquad_noncausal"),
-    FA_CFG_KVQUAD(39, 1, 0, 128, "bm64_bn64_w8_m16_kvquad_causal"),
-    FA_CFG_KVQUAD(40, 0, 1, 128, "bf16_bm64_bn64_w8_m16_kvquad_noncausal"),
-    FA_CFG_KVQUAD(41, 1, 1, 128, "bf16_bm64_bn64_w8_m16_kvquad_causal"),
-    FA_CFG_KVQUAD(42, 0, 0, 64, "d64_bm64_bn64_w8_m16_kvquad_noncausal"),
-    FA_CFG_KVQUAD(43, 1, 0, 64, "d64_bm64_bn64_w8_m16_kvquad_causal"),
-    FA_CFG_KVQUAD(44, 0, 1, 64, "bf16_d64_bm64_bn64_w8_m16_kvquad_noncausal"),
-    FA_CFG_KVQUAD(45, 1, 1, 64, "bf16_d64_bm64_bn64_w8_m16_kvquad_causal"),
-    // 64 query rows per wave (QB = 4), per-item and persistent
-    FA_CFG_W4X64(46, 0, 0, 0, "bm256_bn64_w4x64_m16_noncausal"),
-    FA_CFG_W4X64(47, 1, 0, 0, "bm256_bn64_w4x64_m16_causal"),
-    FA_CFG_W4X64(48, 0, 2, 0, "bm256_bn64_w4x64_m16_persistent_noncausal"),
-    FA_CFG_W4X64(49, 1, 2, 0, "bm256_bn64_w4x64_m16_persistent_causal"),
+    FA_CFG_KVQUAD(30, 0, 0, 128, "bm64_bn64_w8_m16_kvquad_noncausal"),
+    FA_CFG_KVQUAD(31, 1, 0, 128, "bm64_bn64_w8_m16_kvquad_causal"),
+    FA_CFG_KVQUAD(32, 0, 1, 128, "bf16_bm64_bn64_w8_m16_kvquad_noncausal"),
+    FA_CFG_KVQUAD(33, 1, 1, 128, "bf16_bm64_bn64_w8_m16_kvquad_causal"),
+    FA_CFG_KVQUAD(34, 0, 0, 64, "d64_bm64_bn64_w8_m16_kvquad_noncausal"),
+    FA_CFG_KVQUAD(35, 1, 0, 64, "d64_bm64_bn64_w8_m16_kvquad_causal"),
+    FA_CFG_KVQUAD(36, 0, 1, 64, "bf16_d64_bm64_bn64_w8_m16_kvquad_noncausal"),
+    FA_CFG_KVQUAD(37, 1, 1, 64, "bf16_d64_bm64_bn64_w8_m16_kvquad_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -475,14 +437,6 @@ static int prepare(int id) {
   return errs[dev][id] == hipSuccess ? FA_OK : FA_ERR_HIP;
 }
 
-// causal rank-band width (query blocks of one head kept together on an XCD).
-// No run-time override in the product library: tuning builds set
-// -DFA_CAUSAL_BAND=<n> (1 = plain heaviest-first order), e.g.
-// `make variant-band16 VFLAGS=-DFA_CAUSAL_BAND=16`.
-#ifndef FA_CAUSAL_BAND
-#define FA_CAUSAL_BAND 0  // 0 = automatic
-#endif
-static_assert(FA_CAUSAL_BAND >= 0, "FA_CAUSAL_BAND: 0 (automatic) or a band width >= 1");
 
 // CUs of the current device (cached per device id)
 static int num_cus() {
@@ -532,7 +486,7 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   p.c = p.scale * 1.4426950408889634f;        // LOG2E, ref :239
   // few heads per XCD: plain heaviest-first balances better; many: keep the
   // query blocks of a head together for L2 reuse (profiles/r01_band_ab.txt)
-  p.band = FA_CAUSAL_BAND > 0 ? FA_CAUSAL_BAND : (bh <= 64 ? 1 : 16);
+  p.band = bh <= 64 ? 1 : 16;
   long long blocks = (long long)p.nqb * bh * num_splits;
   if (blocks > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
   if (cfg.kind == 2) {
@@ -547,13 +501,16 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   return hipGetLastError() == hipSuccess ? FA_OK : FA_ERR_LAUNCH;
 }
 
-static int cfg_for(int waves, int bn, int causal, int mfma, int sched, int kind = 0) {
-  for (int i = 0; i < kNumConfigs; ++i)
-    if (kConfigs[i].info.waves == waves && kConfigs[i].info.block_n == bn &&
-        kConfigs[i].info.causal == causal && kConfigs[i].kind == kind &&
-        kConfigs[i].mfma == mfma && kConfigs[i].sched == sched &&
-        kConfigs[i].info.dtype == FA_DTYPE_F16 && kConfigs[i].info.head_dim == 128)
+// the fp16 head_dim-128 config of a tier: (block_m, waves, block_n, mask,
+// schedule, kind) -- every field that tells two tiers apart
+static int cfg_for(int block_m, int waves, int bn, int causal, int sched, int kind) {
+  for (int i = 0; i < kNumConfigs; ++i) {
+    const Config& c = kConfigs[i];
+    if (c.info.block_m == block_m && c.info.waves == waves && c.info.block_n == bn &&
+        c.info.causal == causal && c.kind == kind && c.sched == sched &&
+        c.info.dtype == FA_DTYPE_F16 && c.info.head_dim == 128)
       return i;
+  }
   return -1;
 }
 
@@ -564,10 +521,10 @@ static int twin(int id, int dtype, int head_dim) {
   const Config& c = kConfigs[id];
   for (int i = 0; i < kNumConfigs; ++i) {
     const Config& t = kConfigs[i];
-    if (t.info.dtype == dtype && t.info.head_dim == head_dim && t.info.waves == c.info.waves &&
-        t.info.block_n == c.info.block_n && t.info.causal == c.info.causal &&
-        t.info.split_kv == c.info.split_kv && t.mfma == c.mfma && t.sched == c.sched &&
-        t.kind == c.kind)
+    if (t.info.dtype == dtype && t.info.head_dim == head_dim && t.info.block_m == c.info.block_m &&
+        t.info.waves == c.info.waves && t.info.block_n == c.info.block_n &&
+        t.info.causal == c.info.causal && t.info.split_kv == c.info.split_kv &&
+        t.sched == c.sched && t.kind == c.kind)
       return i;
   }
   return -1;
@@ -626,15 +583,16 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   const long long wg128 = bh * ((seq_len + 127) / 128);
   const long long wg64 = bh * ((seq_len + 63) / 64);
   const long long nqb256 = (seq_len + 255) / 256;
-  if (seq_len <= 128) return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
+  const int c = causal ? 1 : 0;
+  if (seq_len <= 128) return cfg_for(128, 4, 64, c, 0, 0);
   // causal with about one 256-row item per CU: the snake cannot balance item
   // costs 1..nqb256, so the KV-pair's halved heaviest key loop wins from
   // nqb256 = 4 on (B=2 S=1024: 503 vs 461; B=4 S=512: 264 vs 364)
   // non-causal: from 160 items (B=1 H=24 S=2048: 829 vs KV-pair 668; H=6
   // S=8192: 1039 vs 854; at 128 items the KV-pair still wins, 732 vs 532)
   const bool persist = causal ? (wg256 >= 384 || (wg256 >= 256 && nqb256 <= 2)) : wg256 >= 160;
-  if (persist) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 2);
-  if (seq_len <= 256) return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
+  if (persist) return cfg_for(256, 8, 64, c, 1, 2);
+  if (seq_len <= 256) return cfg_for(128, 4, 64, c, 0, 0);
   // causal, two rounds of 64-row blocks over long heads (>= 32 blocks per
   // head): the KV-quad's four-way key split halves the heaviest block's key
   // loop against the KV-pair (B=1 H=4 S=8192 765 vs 599, H=2 S=16384 808 vs
@@ -642,9 +600,9 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   // 512 blocks the KV-pair still wins: profiles/r02_pair_vs_quad.jsonl)
   const long long nqb64 = (seq_len + 63) / 64;
   if (wg64 <= 256 || (causal && wg64 <= 512 && nqb64 >= 32))
-    return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 4);
-  if (wg128 <= 512) return cfg_for(8, 64, causal ? 1 : 0, 16, 1, 3);
-  return cfg_for(4, 64, causal ? 1 : 0, 16, 0);
+    return cfg_for(64, 8, 64, c, 1, 4);
+  if (wg128 <= 512) return cfg_for(128, 8, 64, c, 1, 3);
+  return cfg_for(128, 4, 64, c, 0, 0);
 }
 
 namespace fa {
@@ -688,7 +646,7 @@ extern "C" int fa_fwd_f16(const void* q, const void* k, const void* v, void* o, 
 }
 
 // ---- split-KV ---------------------------------------------------------------
-static int splitkv_cfg(int causal) { return causal ? 13 : 12; }
+static int splitkv_cfg(int causal) { return cfg_for(128, 4, 64, causal ? 1 : 0, 0, 1); }
 
 extern "C" int fa_splitkv_num_splits(int batch, int heads, int seq_len, int causal) {
   // enough workgroups to cover 256 CUs twice, at most one split per key tile

@@ -29,10 +29,10 @@
 //  * Causal: waves skip key tiles entirely above their diagonal; the block
 //    ordering (heaviest first, XCD-aware) lives in fa_fwd.hip.
 //
-// Two MFMA shapes share the skeleton (policy classes below):
-//  * M32: v_mfma_f32_32x32x16_f16, one 32-query block per wave.
-//  * M16: v_mfma_f32_16x16x32_f16, two 16-query blocks per wave (the shape
-//    that holds the higher clock under load, profiles/r01_mfma_rate_probe.jsonl).
+// The tile math is the M16 policy below: v_mfma_f32_16x16x32_f16, two
+// 16-query blocks per wave (the shape that holds the higher clock under load,
+// profiles/r01_mfma_rate_probe.jsonl).  The one-wave-per-SIMD persistent
+// kernel (64 rows per wave, asm-owned register file) is fa_w4_kernel.hpp.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -54,13 +54,16 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 constexpr int HD = 128;            // head_dim (the reference hard-codes 128, :613)
 constexpr int ROW_BYTES = HD * 2;  // one K/V/Q row in bytes
 constexpr float RESCALE_LOG2 = 8.0f;
-// attention_kvpair: 4 tile buffers (64 KB) or the merge region (4 x 17 KB at head_dim 128)
-#ifndef FA_KVPAIR_SHARE_Q
-#define FA_KVPAIR_SHARE_Q 1
+// The product library is built from these sources as they stand: no build
+// flag may change what a kernel computes.  Timing-only diagnostic builds
+// (wrong results by design) live in git history, not behind macros here.
+#if defined(FA_DIAG_NO_LDS) || defined(FA_DIAG_NO_MERGE) || defined(FA_DIAG_W4_NO_STAGE) || \
+    defined(FA_DIAG_FREE_CONTRACT) || defined(FA_NARROW_STORE) || defined(FA_ROWSUM_VALU)
+#error "removed A/B knob: the product sources take no result-changing -D flags"
 #endif
-constexpr int kKvpairLdsBytes =
-    FA_KVPAIR_SHARE_Q ? 4 * 64 * 256 + 4 * 8 * 64 * 16  // 4 tile buffers + shared Q (4 x 8 KB)
-                      : 4 * (2 * 8 + 1) * 64 * 16;      // 4 tile buffers or the merge region
+// attention_kvpair: 4 tile buffers (64 KB) + the shared Q block (4 x 8 KB);
+// the merge region reuses the tile buffers
+constexpr int kKvpairLdsBytes = 4 * 64 * 256 + 4 * 8 * 64 * 16;
 // KV-quad: four double-width (128-key) stage buffers
 constexpr int kKvquadLdsBytes = 4 * 2 * 64 * 256;
 
@@ -183,29 +186,15 @@ __device__ __forceinline__ float ninf() { return -__builtin_inff(); }
 // O stored right after the last PV).  With half the MFMAs per tile the MFMA
 // phase is the short one at d64, the reverse of d128; +15-20 % at S=2048-16384
 // fp16 and bf16, bit-identical (profiles/r02_ab_d64_noncausal_sched.jsonl).
-// The knobs restore the d128 non-causal choices (1, 0, 0) for A/B.
-#ifndef FA_NC_D64_ISSUE_IN_SM
-#define FA_NC_D64_ISSUE_IN_SM 0
-#endif
-#ifndef FA_NC_D64_WRITE_EARLY
-#define FA_NC_D64_WRITE_EARLY 1
-#endif
-#ifndef FA_NC_D64_EARLY_STORE
-#define FA_NC_D64_EARLY_STORE 1
-#endif
-#ifndef FA_O_STORE_AUX
-#define FA_O_STORE_AUX 16
-#endif
+constexpr bool kNcD64IssueInSm = false;
+constexpr bool kNcD64WriteEarly = true;
+constexpr bool kNcD64EarlyStore = true;
+constexpr int kOStoreAux = 16;
 
 // 32-bit LDS address of a pointer into the workgroup's shared memory
 __device__ __forceinline__ int lds_addr(const void* p) {
   return (int)(unsigned)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
 }
-
-#ifndef FA_W4_TILE_INC
-#define FA_W4_TILE_INC "fa_w4_tile_asm.inc"  // diagnostic builds swap in a variant
-#endif
-#include FA_W4_TILE_INC  // w4_tile_asm: hand-scheduled W4x64 tile body
 
 #ifdef FA_STAMPS
 // diagnostic build only (lib/libfa_mi355x_stamps.so): per-wave cycles spent in
@@ -226,217 +215,7 @@ __device__ unsigned long long g_fa_timeline[FA_MAX_TIMELINE][4];  // + shader cy
 //   pv(vb)       : O^T += V^T . P^T          (MFMA, V tile from LDS)
 // so the ping-pong skeleton can pair one wave's MFMA block with its SIMD
 // partner's softmax.
-//
-// M32: v_mfma_f32_32x32x16_f16, one 32-query block per wave
-//   S^T[cb] (32 keys x 32 q): lane holds q = lane&31, keys 32cb+(i&3)+8(i>>2)+4h
-//   O^T[e]  (32 d x 32 q):   lane holds q = lane&31, d = 32e+(i&3)+8(i>>2)+4h
-// Both tiles use LDS image A.
 // ---------------------------------------------------------------------------
-template <int BN_>
-struct M32 {
-  static constexpr int BN = BN_;
-  static constexpr int HDIM = 128;  // head_dim 128 only
-  static constexpr int RPW = 4;     // tile rows one wave stages per pass
-  static constexpr int NSB = BN / 32;  // 32-key S^T blocks per tile
-  static constexpr int RW = 32;        // query rows per wave
-  int lane, r, h;
-  int kaddr0, kaddr1, vaddr0, vaddr1;
-  f16x8 qf[8];
-  f32x16 acc[4];
-  f32x16 s[NSB];
-  f16x8 pf[BN / 16];
-  f32x16 negm;    // C operand of the QK^T chains: -m_ref broadcast
-  f32x16 lacc;    // running row sums (ones . P in the PV chain); every register = l(q)
-  float m_ref;    // reference max, log2 units (x = s*c - m_ref)
-  bool have_ref;  // wave-uniform: a tile has set m_ref
-  float c;
-
-  __device__ __forceinline__ void init(int lane_, float c_) {
-    lane = lane_;
-    c = c_;
-    r = lane & 31;
-    h = lane >> 5;
-    // K row read (A of S^T): row 32cb+r, chunk 2t+h -> 8192cb + 512(t>>1) + kaddr[t&1]
-    kaddr0 = lds_off(r, h);
-    kaddr1 = lds_off(r, 2 + h);
-    // V transposed read (A of O^T): group G=lane>>4, i=lane&15=4qq+pp, rows
-    // 32cb+16s+8m+4h+qq, cols 32e+16(G&1)+4pp -> 8192cb+4096s+512e + vaddr[m]
-    const int G = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
-    const int base = 64 * (4 * h + qq) + 8 * (pp & 1);
-    vaddr0 = base + 16 * ((2 * (G & 1) + (pp >> 1)) ^ h);
-    vaddr1 = 2048 + base + 16 * ((2 * (G & 1) + (pp >> 1)) ^ (2 + h));
-#pragma unroll
-    for (int e = 0; e < 4; ++e) acc[e] = f32x16{};
-    negm = f32x16{};
-    lacc = f32x16{};
-    m_ref = 0.f;
-    have_ref = false;
-  }
-  // Q (B operand of S^T): lane holds c * Q[qw + r][16t + 8h .. +7]  (fp16)
-  __device__ __forceinline__ void issue_q(__amdgpu_buffer_rsrc_t rq, int qw) {
-#pragma unroll
-    for (int t = 0; t < 8; ++t) qf[t] = buf_load16(rq, (qw + r) * ROW_BYTES + (2 * t + h) * 16);
-  }
-  __device__ __forceinline__ void scale_q() {
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[t][j] = (f16)((float)qf[t][j] * c);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) asm volatile("" : "+v"(qf[t]));  // see M16::pin_q
-  }
-  __device__ __forceinline__ void load_q(__amdgpu_buffer_rsrc_t rq, int qw) {
-    issue_q(rq, qw);
-    scale_q();
-  }
-  // staging: 8 consecutive lanes = two rows of opposite parity x 4 chunks
-  // (conflict-free ds_write_b128 into image A)
-  __device__ __forceinline__ int k_stage_row(int wave) const {
-    return 4 * wave + 2 * ((lane >> 5) & 1) + ((lane >> 2) & 1);
-  }
-  __device__ __forceinline__ int k_stage_ch() const { return 4 * ((lane >> 3) & 3) + (lane & 3); }
-  __device__ __forceinline__ int v_stage_row(int wave) const { return k_stage_row(wave); }
-  __device__ __forceinline__ int v_stage_ch() const { return k_stage_ch(); }
-  static __device__ __forceinline__ int k_lds(int row, int ch) { return lds_off(row, ch); }
-  static __device__ __forceinline__ int v_lds(int row, int ch) { return lds_off(row, ch); }
-
-  __device__ __forceinline__ void qk(const char* kb) {
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int ka = ((t & 1) ? kaddr1 : kaddr0) + 512 * (t >> 1);
-#pragma unroll
-      for (int cb = 0; cb < NSB; ++cb) {
-        const f16x8 kf = *reinterpret_cast<const f16x8*>(kb + ka + 8192 * cb);
-        s[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[t], t == 0 ? negm : s[cb], 0, 0, 0);
-      }
-    }
-  }
-  template <bool CAUSAL>
-  __device__ __forceinline__ void softmax(int kv0, int kv_hi, int qw, float /*c*/, bool need_mask) {
-    if (need_mask) {
-      const int qrow = qw + r;
-#pragma unroll
-      for (int cb = 0; cb < NSB; ++cb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int kv = kv0 + 32 * cb + (i & 3) + 8 * (i >> 2) + 4 * h;
-          const bool ok = kv < kv_hi && (!CAUSAL || kv <= qrow);
-          s[cb][i] = ok ? s[cb][i] : ninf();
-        }
-    }
-    // row max relative to m_ref; move m_ref only when it grew by > RESCALE_LOG2
-    float mx = s[0][0];
-#pragma unroll
-    for (int cb = 0; cb < NSB; ++cb)
-#pragma unroll
-      for (int i = (cb == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, s[cb][i]);
-    mx = max_xor32(mx);
-    if (__any(!have_ref || mx > RESCALE_LOG2)) {
-      // first tile: centre on the max; later: only ever move m_ref up.
-      // A row with every key masked (mx = -inf) keeps m_ref.
-      float sh = have_ref ? fmaxf(mx, 0.f) : mx;
-      sh = sh == ninf() ? 0.f : sh;
-      if (have_ref) {
-        const float alpha = __builtin_amdgcn_exp2f(-sh);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] *= alpha;
-        lacc *= alpha;
-      }
-#pragma unroll
-      for (int cb = 0; cb < NSB; ++cb) s[cb] -= sh;
-      m_ref += sh;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) negm[i] = -m_ref;
-      have_ref = true;
-    }
-#pragma unroll
-    for (int cb = 0; cb < NSB; ++cb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) pf[2 * cb + (i >> 3)][i & 7] = (f16)__builtin_amdgcn_exp2f(s[cb][i]);
-  }
-  __device__ __forceinline__ void pv(const char* vb) {
-    const f16x8 ones = {(f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1, (f16)1};
-#pragma unroll
-    for (int u = 0; u < BN / 16; ++u) {
-      const int cb = u >> 1, sb = u & 1;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int imm = 8192 * cb + 4096 * sb + 512 * e;
-        const f16x4 lo = lds_read_tr(vb, vaddr0 + imm);
-        const f16x4 hi = lds_read_tr(vb, vaddr1 + imm);
-        const f16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        acc[e] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[u], acc[e], 0, 0, 0);
-      }
-      lacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ones, pf[u], lacc, 0, 0, 0);
-    }
-  }
-  template <bool CAUSAL>
-  __device__ __forceinline__ void tile(const char* kb, const char* vb, int kv0, int kv_hi, int qw,
-                                       float c_, bool need_mask) {
-    qk(kb);
-    softmax<CAUSAL>(kv0, kv_hi, qw, c_, need_mask);
-    pv(vb);
-  }
-  __device__ __forceinline__ void mfma_block(const char* kb, const char* vb, bool do_pv, bool do_qk) {
-    if (do_pv) {
-      pv(vb);
-#ifdef FA_M32_PIPE
-      // V reads run FA_M32_PIPE ahead: then two per MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, FA_M32_PIPE, 0);
-#pragma unroll
-      for (int i = 0; i < (32 - FA_M32_PIPE) / 2; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 20, 0);
-#endif
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (do_qk) {
-      qk(kb);
-#ifdef FA_M32_PIPE
-      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-#endif
-    }
-  }
-
-  // lane holds O^T[d = 32e + (i&3) + 8(i>>2) + 4h][q = qw + r]
-  __device__ __forceinline__ void store_o(__amdgpu_buffer_rsrc_t ro, int qw) {
-    const float lt = lacc[0];
-    const float inv = lt > 0.f ? 1.0f / lt : 0.f;
-    const int rowb = (qw + r) * ROW_BYTES;
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        f16x4 w;
-#pragma unroll
-        for (int x = 0; x < 4; ++x) w[x] = (f16)(acc[e][4 * g + x] * inv);
-        buf_store8(ro, rowb + 2 * (32 * e + 8 * g + 4 * h), w);
-      }
-  }
-  // m in the reference's units (scaled score, natural log): m_ref * ln 2
-  __device__ __forceinline__ void store_partial(__amdgpu_buffer_rsrc_t rpo, float* pml, int qw,
-                                                int S, float /*scale*/) {
-    const float lt = lacc[0];
-    const int rowb = (qw + r) * HD * 4;
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        buf_store16f(rpo, rowb + 4 * (32 * e + 8 * g + 4 * h),
-                     f32x4{acc[e][4 * g], acc[e][4 * g + 1], acc[e][4 * g + 2], acc[e][4 * g + 3]});
-    if (h == 0 && qw + r < S)
-      *reinterpret_cast<float2*>(pml + (size_t)(qw + r) * 2) =
-          make_float2(lt > 0.f ? m_ref * 0.6931471805599453f : ninf(), lt);
-  }
-};
 
 // ---------------------------------------------------------------------------
 // M16: v_mfma_f32_16x16x32_f16, two 16-query blocks b per wave
@@ -476,6 +255,7 @@ struct Elem {
 
 template <int BN_, class T = f16, int HDIM_ = 128, int QB_ = 2>
 struct M16 {
+  static_assert(QB_ == 2, "two 16-row query blocks per wave (the merge layouts assume it)");
   static_assert(HDIM_ == 64 || HDIM_ == 128, "head_dim 64 or 128");
   static constexpr int BN = BN_;
   static constexpr int HDIM = HDIM_;      // head_dim
@@ -488,7 +268,7 @@ struct M16 {
   // the head_dim-128 one.
   static constexpr int NKB = BN / 16;  // 16-key blocks per tile
   static constexpr int NU = BN / 32;   // 32-key PV steps per tile
-  static constexpr int QB = QB_;       // 16-row query blocks per wave (2: 32 rows, 4: 64 rows)
+  static constexpr int QB = QB_;       // 16-row query blocks per wave (32 rows)
   static constexpr int RW = 16 * QB;   // query rows per wave
   typedef typename Elem<T>::x8 tx8;
   typedef typename Elem<T>::x4 tx4;
@@ -589,66 +369,7 @@ struct M16 {
 #pragma unroll
     for (int b = 0; b < QB; ++b)
 #pragma unroll
-      for (int t = 0; t < NTQ; ++t) {
-        if constexpr (kAsm)
-          asm volatile("" : "+a"(qf[b][t]));
-        else
-          asm volatile("" : "+v"(qf[b][t]));
-      }
-  }
-  // ---- QB = 4: 64 query rows per wave, one wave per SIMD (512 registers) ----
-  // hipcc left to itself routes the S tile through AGPRs (a v_accvgpr copy
-  // per element and pass) and spills (tools/experiments/w4_spill_probe.sh).
-  // Here every MFMA is an inline-asm statement with pinned register classes:
-  // O, l and Q in AGPRs ("a"), S and P in VGPRs ("v").  hipcc pads nothing
-  // inside asm, so the hazards are padded in the statements:
-  //  * "s_nop 2" ahead of each MFMA: a VALU-written operand (P, negm, an
-  //    accvgpr-written O) needs its wait states; between back-to-back MFMAs
-  //    the nop issues in the matrix pipe's shadow;
-  //  * mfma_pad_*: 18 wait states between the last MFMA writing S (or O)
-  //    and the first VALU reading it, ordered through "+v"/"+a" operands.
-  static constexpr bool kAsm = QB == 4;
-  static_assert(!kAsm || std::is_same<T, f16>::value, "asm MFMA path: fp16");
-  __device__ __forceinline__ void mfma_pad_s() {
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 1"
-                 : "+v"(s[0][0]), "+v"(s[0][1]), "+v"(s[0][2]), "+v"(s[0][3]), "+v"(s[1][0]),
-                   "+v"(s[1][1]), "+v"(s[1][2]), "+v"(s[1][3]), "+v"(s[2][0]), "+v"(s[2][1]),
-                   "+v"(s[2][2]), "+v"(s[2][3]), "+v"(s[3][0]), "+v"(s[3][1]), "+v"(s[3][2]),
-                   "+v"(s[3][3]));
-  }
-  // S block = K . Q^T step: first of a chain (C = -m_ref) or accumulate
-  __device__ __forceinline__ void mma_s0(f32x4& d, tx8 kf, const tx8& q, f32x4 c) {
-    if constexpr (kAsm)
-      asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %3" : "=&v"(d) : "v"(kf), "a"(q), "v"(c));
-    else
-      d = Elem<T>::mfma(kf, q, c);
-  }
-  __device__ __forceinline__ void mma_s(f32x4& d, tx8 kf, const tx8& q) {
-    if constexpr (kAsm)
-      asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(d) : "v"(kf), "a"(q));
-    else
-      d = Elem<T>::mfma(kf, q, d);
-  }
-  // O (or l) += V^T-fragment . P
-  __device__ __forceinline__ void mma_o(f32x4& d, tx8 vf, const tx8& p) {
-    if constexpr (kAsm)
-      asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(d) : "v"(vf), "v"(p));
-    else
-      d = Elem<T>::mfma(vf, p, d);
-  }
-  __device__ __forceinline__ void mfma_pad_o() {
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 1"
-                 : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[0][2]), "+a"(acc[0][3]),
-                   "+a"(acc[0][4]), "+a"(acc[0][5]), "+a"(acc[0][6]), "+a"(acc[0][7]),
-                   "+a"(acc[1][0]), "+a"(acc[1][1]), "+a"(acc[1][2]), "+a"(acc[1][3]),
-                   "+a"(acc[1][4]), "+a"(acc[1][5]), "+a"(acc[1][6]), "+a"(acc[1][7]),
-                   "+a"(lacc[0]), "+a"(lacc[1]));
-    asm volatile(""
-                 : "+a"(acc[2][0]), "+a"(acc[2][1]), "+a"(acc[2][2]), "+a"(acc[2][3]),
-                   "+a"(acc[2][4]), "+a"(acc[2][5]), "+a"(acc[2][6]), "+a"(acc[2][7]),
-                   "+a"(acc[3][0]), "+a"(acc[3][1]), "+a"(acc[3][2]), "+a"(acc[3][3]),
-                   "+a"(acc[3][4]), "+a"(acc[3][5]), "+a"(acc[3][6]), "+a"(acc[3][7]),
-                   "+a"(lacc[2]), "+a"(lacc[3]));
+      for (int t = 0; t < NTQ; ++t) asm volatile("" : "+v"(qf[b][t]));
   }
   __device__ __forceinline__ void load_q(__amdgpu_buffer_rsrc_t rq, int qw) {
     issue_q(rq, qw);
@@ -675,36 +396,11 @@ struct M16 {
   static __device__ __forceinline__ int v_src(int o) { return lds_off_src(o); }
 
   __device__ __forceinline__ void qk(const char* kb) {
-    if constexpr (kAsm) {
-#pragma unroll
-      for (int t = 0; t < NTQ; ++t)
-#pragma unroll
-        for (int cb = 0; cb < NKB; ++cb) {
-          const tx8 kf = *reinterpret_cast<const tx8*>(kb + kaddr[t] + 4096 * cb);
-#pragma unroll
-          for (int b = 0; b < QB; ++b) {
-            if (t == 0)
-              asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %3"
-                  : "=&v"(s[b][cb])
-                  : "v"(kf), "a"(qf[b][t]), "v"(negm[b]));
-            else
-              asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0"
-                  : "+v"(s[b][cb])
-                  : "v"(kf), "a"(qf[b][t]));
-          }
-        }
-      mfma_pad_s();
-      return;
-    }
 #pragma unroll
     for (int t = 0; t < NTQ; ++t)
 #pragma unroll
       for (int cb = 0; cb < NKB; ++cb) {
-#ifdef FA_DIAG_NO_LDS  // diagnostic timing build only: operands from registers
-        const tx8 kf = qf[cb & 1][(t + cb) & (NTQ - 1)];
-#else
         const tx8 kf = *reinterpret_cast<const tx8*>(kb + kaddr[t] + 4096 * cb);
-#endif
 #pragma unroll
         for (int b = 0; b < QB; ++b)
           s[b][cb] = Elem<T>::mfma(kf, qf[b][t], t == 0 ? negm[b] : s[b][cb]);
@@ -717,14 +413,7 @@ struct M16 {
 #pragma unroll
       for (int cb = 0; cb < NKB; ++cb)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-        {
-          const float e = __builtin_amdgcn_exp2f(s[b][cb][i]);
-#ifdef FA_ROWSUM_VALU
-          lacc[b][0] += e;  // this lane's partial row sum (4 lanes per row)
-#endif
-          pf[b][cb >> 1][4 * (cb & 1) + i] = (T)e;
-        }
+        for (int i = 0; i < 4; ++i) pf[b][cb >> 1][4 * (cb & 1) + i] = (T)__builtin_amdgcn_exp2f(s[b][cb][i]);
   }
   template <bool CAUSAL>
   __device__ __forceinline__ void softmax(int kv0, int kv_hi, int qw, float /*c*/, bool need_mask) {
@@ -753,21 +442,15 @@ struct M16 {
       for (int cb = 0; cb < NKB; ++cb)
 #pragma unroll
         for (int i = (cb == 0 ? 1 : 0); i < 4; ++i) m = fmaxf(m, s[b][cb][i]);
-#ifdef FA_ROWMAX_ALWAYS
-      mx[b] = max_xor32(max_xor16(m));
-#else
       // a row's max exceeds the threshold iff one of its 4 lanes' partial
       // maxima does: the cross-lane reduction is only needed on the rare
       // (wave-uniform) rescale path
       mx[b] = m;
-#endif
       grow |= mx[b] > RESCALE_LOG2;
     }
     if (__any(grow)) {
-#ifndef FA_ROWMAX_ALWAYS
 #pragma unroll
       for (int b = 0; b < QB; ++b) mx[b] = max_xor32(max_xor16(mx[b]));
-#endif
 #pragma unroll
       for (int b = 0; b < QB; ++b) {
         // first tile: centre on the max; later: only ever move m_ref up.
@@ -775,9 +458,6 @@ struct M16 {
         float sh = have_ref ? fmaxf(mx[b], 0.f) : mx[b];
         sh = sh == ninf() ? 0.f : sh;
         if (have_ref) {
-          if constexpr (kAsm) {
-            if (b == 0) mfma_pad_o();
-          }
           const float alpha = __builtin_amdgcn_exp2f(-sh);
 #pragma unroll
           for (int e = 0; e < NE; ++e) acc[b][e] *= alpha;
@@ -792,247 +472,36 @@ struct M16 {
     }
     exp_p();
   }
-  // ---- split softmax for the one-wave-per-SIMD pipeline (attention_w4) ----
-  // softmax(j) runs beside PV(j-1) and is cut where its rare, wave-uniform
-  // rescale decision sits:
-  //   sm_max   : mask, per-lane partial row maxima, "some row grew" flag
-  //   sm_shift : (rare) move m_ref, shift S, remember alpha for O and l
-  //   sm_exp   : P = exp2(S) in place (fp32, still in the S registers)
-  //   sm_alpha : (rare) O, l *= alpha -- after PV(j-1) has accumulated,
-  //              since that tile's P was relative to the old m_ref
-  //   cvt_p    : S -> fp16 P (the PV B operand), beside QK^T(j+1), whose
-  //              MFMAs then overwrite the S registers
-  float alpha[QB];
-  template <bool CAUSAL>
-  __device__ __forceinline__ bool sm_max(int kv0, int kv_hi, int qw, bool need_mask) {
-    if (need_mask) {
-#pragma unroll
-      for (int b = 0; b < QB; ++b) {
-        const int qrow = qw + 16 * b + r16;
-#pragma unroll
-        for (int cb = 0; cb < NKB; ++cb)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int kv = kv0 + 16 * cb + 4 * sg + i;
-            const bool ok = kv < kv_hi && (!CAUSAL || kv <= qrow);
-            s[b][cb][i] = ok ? s[b][cb][i] : ninf();
-          }
-      }
-    }
-    bool grow = !have_ref;
-#pragma unroll
-    for (int b = 0; b < QB; ++b) {
-      float m = s[b][0][0];
-#pragma unroll
-      for (int cb = 0; cb < NKB; ++cb)
-#pragma unroll
-        for (int i = (cb == 0 ? 1 : 0); i < 4; ++i) m = fmaxf(m, s[b][cb][i]);
-      mx_[b] = m;
-      grow |= m > RESCALE_LOG2;
-    }
-    return __any(grow);
-  }
-  float mx_[QB];
-  // returns true when O and l must be rescaled (sm_alpha) after PV(j-1)
-  __device__ __forceinline__ bool sm_shift() {
-    const bool had = have_ref;
-#pragma unroll
-    for (int b = 0; b < QB; ++b) {
-      const float mxb = max_xor32(max_xor16(mx_[b]));
-      // first tile: centre on the max; later: only ever move m_ref up.
-      // A row with every key masked (mx = -inf) keeps m_ref.
-      float sh = had ? fmaxf(mxb, 0.f) : mxb;
-      sh = sh == ninf() ? 0.f : sh;
-      alpha[b] = __builtin_amdgcn_exp2f(-sh);
-#pragma unroll
-      for (int cb = 0; cb < NKB; ++cb) s[b][cb] -= sh;
-      m_ref[b] += sh;
-      negm[b] = f32x4{-m_ref[b], -m_ref[b], -m_ref[b], -m_ref[b]};
-    }
-    have_ref = true;
-    return had;
-  }
-  __device__ __forceinline__ void sm_exp() {
-#pragma unroll
-    for (int b = 0; b < QB; ++b)
-#pragma unroll
-      for (int cb = 0; cb < NKB; ++cb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) s[b][cb][i] = __builtin_amdgcn_exp2f(s[b][cb][i]);
-  }
-  // x *= a for an accumulator tuple; asm path: through 4 VGPRs and back into
-  // the same AGPR class, one tuple at a time
-  __device__ __forceinline__ void scale_acc(f32x4& x, float a) {
-    if constexpr (kAsm) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float t;
-        asm volatile(
-            "v_accvgpr_read_b32 %1, %0\n\t"
-            "v_mul_f32_e32 %1, %1, %2\n\t"
-            "v_accvgpr_write_b32 %0, %1"
-            : "+a"(x[i]), "=&v"(t)
-            : "v"(a));
-      }
-    } else {
-      x *= a;
-    }
-  }
-  // one 4-register accumulator tuple at a time (sched_barrier): scheduled
-  // freely, hipcc reads all 144 AGPRs ahead of the multiplies and the
-  // temporaries spill the pipelined loop
-  __device__ __forceinline__ void sm_alpha() {
-    if constexpr (kAsm) mfma_pad_o();
-#pragma unroll
-    for (int b = 0; b < QB; ++b) {
-#pragma unroll
-      for (int e = 0; e < NE; ++e) scale_acc(acc[b][e], alpha[b]);
-      scale_acc(lacc[b], alpha[b]);
-    }
-  }
-  // W4 pipeline with P double-buffered (P(j) is written beside the PV(j-1)
-  // MFMAs that read P(j-1)): buffer PB of {pf, pf2}
-  tx8 pf2[QB][NU];
-  template <int PB>
-  __device__ __forceinline__ tx8 (&pbuf())[QB][NU] {
-    if constexpr (PB == 0) return pf; else return pf2;
-  }
-  template <int PB>
-  __device__ __forceinline__ void exp_cvt() {
-    tx8 (&P)[QB][NU] = pbuf<PB>();
-#pragma unroll
-    for (int b = 0; b < QB; ++b)
-#pragma unroll
-      for (int cb = 0; cb < NKB; ++cb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) P[b][cb >> 1][4 * (cb & 1) + i] = (T)__builtin_amdgcn_exp2f(s[b][cb][i]);
-  }
-  template <int PB>
-  __device__ __forceinline__ void pv_buf(const char* vb) {
-    tx8 (&P)[QB][NU] = pbuf<PB>();
-    const tx8 ones = {(T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f};
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-#pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        const int base = 8192 * u + 512 * (e >> 1) + vaddr[e & 1];
-        const tx4 lo = __builtin_bit_cast(tx4, lds_read_tr(vb, base));
-        const tx4 hi = __builtin_bit_cast(tx4, lds_read_tr(vb, base + 4096));
-        const tx8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-#pragma unroll
-        for (int b = 0; b < QB; ++b) mma_o(acc[b][e], vf, P[b][u]);
-      }
-#pragma unroll
-      for (int b = 0; b < QB; ++b) mma_o(lacc[b], ones, P[b][u]);
-    }
-  }
-  // chain-major QK^T: each S block's 4-deep chain back to back (a dependent
-  // 16x16x32 chain issues at full rate), so S blocks complete one by one and
-  // their row maxima can start beside the remaining MFMAs
-  __device__ __forceinline__ void qk_cm(const char* kb) {
-#pragma unroll
-    for (int cb = 0; cb < NKB; ++cb) {
-      tx8 kf[NTQ];
-#pragma unroll
-      for (int t = 0; t < NTQ; ++t) kf[t] = *reinterpret_cast<const tx8*>(kb + kaddr[t] + 4096 * cb);
-#pragma unroll
-      for (int b = 0; b < QB; ++b)
-#pragma unroll
-        for (int t = 0; t < NTQ; ++t) {
-          if (t == 0) mma_s0(s[b][cb], kf[t], qf[b][t], negm[b]);
-          else mma_s(s[b][cb], kf[t], qf[b][t]);
-        }
-    }
-    if constexpr (kAsm) mfma_pad_s();
-  }
-  __device__ __forceinline__ void cvt_p() {
-#pragma unroll
-    for (int b = 0; b < QB; ++b)
-#pragma unroll
-      for (int cb = 0; cb < NKB; ++cb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pf[b][cb >> 1][4 * (cb & 1) + i] = (T)s[b][cb][i];
-  }
-
-  // one 32-key half (u) of the PV product and its row-sum MFMAs
-  __device__ __forceinline__ void pv_half(const char* vb, int u) {
-    const tx8 ones = {(T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f};
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      const int base = 8192 * u + 512 * (e >> 1) + vaddr[e & 1];
-      const tx4 lo = __builtin_bit_cast(tx4, lds_read_tr(vb, base));
-      const tx4 hi = __builtin_bit_cast(tx4, lds_read_tr(vb, base + 4096));
-      const tx8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-#pragma unroll
-      for (int b = 0; b < QB; ++b) mma_o(acc[b][e], vf, pf[b][u]);
-    }
-#pragma unroll
-    for (int b = 0; b < QB; ++b) mma_o(lacc[b], ones, pf[b][u]);
-  }
   __device__ __forceinline__ void pv(const char* vb) {
     const tx8 ones = {(T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f};
-    if constexpr (kAsm) {
-#pragma unroll
-      for (int u = 0; u < NU; ++u) {
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-          const int base = 8192 * u + 512 * (e >> 1) + vaddr[e & 1];
-          const tx4 lo = __builtin_bit_cast(tx4, lds_read_tr(vb, base));
-          const tx4 hi = __builtin_bit_cast(tx4, lds_read_tr(vb, base + 4096));
-          const tx8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-#pragma unroll
-          for (int b = 0; b < QB; ++b)
-            asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0"
-                : "+a"(acc[b][e])
-                : "v"(vf), "v"(pf[b][u]));
-        }
-#pragma unroll
-        for (int b = 0; b < QB; ++b)
-          asm("s_nop 2\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0"
-              : "+a"(lacc[b])
-              : "v"(ones), "v"(pf[b][u]));
-      }
-      return;
-    }
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
 #pragma unroll
       for (int e = 0; e < NE; ++e) {
-#ifdef FA_DIAG_NO_LDS
-        const tx8 vf = qf[e & 1][(u + e) & (NTQ - 1)];
-#else
         const int base = 8192 * u + 512 * (e >> 1) + vaddr[e & 1];
         const tx4 lo = __builtin_bit_cast(tx4, lds_read_tr(vb, base));
         const tx4 hi = __builtin_bit_cast(tx4, lds_read_tr(vb, base + 4096));
         const tx8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-#endif
 #pragma unroll
         for (int b = 0; b < QB; ++b)
           acc[b][e] = Elem<T>::mfma(vf, pf[b][u], acc[b][e]);
       }
       // row sums of the same fp16 P: every register of lacc[b] = l for q = lane&15
-#ifndef FA_ROWSUM_VALU
 #pragma unroll
       for (int b = 0; b < QB; ++b)
         lacc[b] = Elem<T>::mfma(ones, pf[b][u], lacc[b]);
-#endif
     }
   }
   // the ping-pong MFMA block: PV(V_{k-1}) then QK^T(K_k); the barrier keeps the
   // scheduler from hoisting QK's LDS reads into PV (register pressure)
+  // LDS reads kept in flight ahead of the MFMAs that consume them: 4 K reads
+  // (A/B +3-6 %), 8 V reads (pins the schedule in every instantiation)
+  static constexpr int kQkPipe = 4, kPvPipe = 8;
   __device__ __forceinline__ void mfma_block(const char* kb, const char* vb, bool do_pv, bool do_qk) {
-#ifndef FA_QK_PIPE
-#define FA_QK_PIPE 4  // K reads kept in flight ahead of the QK^T MFMAs (A/B: +3-6 %)
-#endif
-#ifndef FA_PV_PIPE
-#define FA_PV_PIPE 8  // V reads in flight ahead of the PV MFMAs (pins the schedule in every instantiation)
-#endif
-#if FA_QK_PIPE > 0
     if (do_pv) {
       pv(vb);
-#if FA_PV_PIPE > 0
       constexpr int PV_READS = 2 * NE * NU, PV_MFMAS = 2 * NE * NU + 2 * NU;
-      constexpr int PV_AHEAD = FA_PV_PIPE < PV_READS ? FA_PV_PIPE : PV_READS;
+      constexpr int PV_AHEAD = kPvPipe < PV_READS ? kPvPipe : PV_READS;
       __builtin_amdgcn_sched_group_barrier(0x100, PV_AHEAD, 0);
 #pragma unroll
       for (int i = 0; i < (PV_READS - PV_AHEAD) / 2; ++i) {
@@ -1040,55 +509,30 @@ struct M16 {
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
       __builtin_amdgcn_sched_group_barrier(0x008, PV_MFMAS, 0);
-#endif
     }
     __builtin_amdgcn_sched_barrier(0);
     if (do_qk) {
       qk(kb);
-      // keep FA_QK_PIPE K reads in flight ahead of the MFMAs that consume them
       constexpr int QK_READS = NTQ * NKB;
-      __builtin_amdgcn_sched_group_barrier(0x100, FA_QK_PIPE, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, kQkPipe, 0);
 #pragma unroll
-      for (int i = 0; i < QK_READS - FA_QK_PIPE; ++i) {
+      for (int i = 0; i < QK_READS - kQkPipe; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, 2 * FA_QK_PIPE, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * kQkPipe, 0);
     }
-    return;
-#endif
-    if (do_pv) pv(vb);
-    __builtin_amdgcn_sched_barrier(0);
-    if (do_qk) qk(kb);
   }
   template <bool CAUSAL>
   __device__ __forceinline__ void tile(const char* kb, const char* vb, int kv0, int kv_hi, int qw,
                                        float c_, bool need_mask) {
-#ifdef FA_W4_TILE_ASM  // opt-in: measured level with (non-causal) or 2-4 % below (causal) the plain body
-    if constexpr (kAsm) {
-      // common case: the hand-scheduled tile body (tools/gen_w4_tile_asm.py);
-      // masked tiles, the first tile and a row max past RESCALE_LOG2 (rare)
-      // take the plain path below, which recomputes S from the same LDS tile
-      if (!need_mask && have_ref) {
-        const int kl = lds_addr(kb), vl = lds_addr(vb);
-        const int ka[4] = {kl + kaddr[0], kl + kaddr[1], kl + kaddr[2], kl + kaddr[3]};
-        const int va[2] = {vl + vaddr[0], vl + vaddr[1]};
-        const tx8 ones = {(T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f, (T)1.f};
-        if (!w4_tile_asm(acc, lacc, qf, m_ref, ka, va, ones)) return;
-      }
-    }
-#endif
     qk(kb);
     softmax<CAUSAL>(kv0, kv_hi, qw, c_, need_mask);
     pv(vb);
   }
 
   __device__ __forceinline__ float row_sum(int b) const {
-#ifdef FA_ROWSUM_VALU
-    return sum_xor32(sum_xor16(lacc[b][0]));
-#else
     return lacc[b][0];  // already the full row sum (MFMA over all keys)
-#endif
   }
   // Epilogue: lane (g, r16) holds d = 16e + 4g + 0..3 of row r16 for every e.
   // One v_permlane16_swap per dword of a d-block pair (e, e+1) exchanges the
@@ -1100,21 +544,11 @@ struct M16 {
   // row blocks [B0, B1), d-block pairs [EP0, EP1) (symmetric merges store a part each)
   template <int B0 = 0, int B1 = QB, int EP0 = 0, int EP1 = NE / 2>
   __device__ __forceinline__ void store_o(__amdgpu_buffer_rsrc_t ro, int qw) {
-    if constexpr (kAsm) mfma_pad_o();
 #pragma unroll
     for (int b = B0; b < B1; ++b) {
       const float lt = row_sum(b);  // already the full row sum (MFMA over all keys)
       const float inv = lt > 0.f ? 1.0f / lt : 0.f;
       const int rowb = (qw + 16 * b + r16) * ROW;
-#ifdef FA_NARROW_STORE
-#pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        tx4 w;
-#pragma unroll
-        for (int x = 0; x < 4; ++x) w[x] = (T)(acc[b][e][x] * inv);
-        buf_store8(ro, rowb + 2 * (16 * e + 4 * g), __builtin_bit_cast(f16x4, w));
-      }
-#else
       const int dlane = 16 * (g & 1) + 8 * (g >> 1);
 #pragma unroll
       for (int ep = EP0; ep < EP1; ++ep) {
@@ -1132,70 +566,26 @@ struct M16 {
           Y[dw] = r[1];
         }
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{X[0], X[1], Y[0], Y[1]}, ro,
-                                               rowb + 2 * (32 * ep + dlane), 0, FA_O_STORE_AUX);
+                                               rowb + 2 * (32 * ep + dlane), 0, kOStoreAux);
       }
-#endif
     }
   }
   // a*wa + b*wb with the contraction fixed (fma(a, wa, b*wb)): left to the
   // compiler, which product it fuses depends on which operand arrives from
   // LDS, so two merge paths of the same arithmetic could round differently
   static __device__ __forceinline__ float mix(float a, float wa, float b, float wb) {
-#ifdef FA_DIAG_FREE_CONTRACT  // A/B only: the compiler picks the contraction
-    return a * wa + b * wb;
-#else
     return __builtin_fmaf(a, wa, b * wb);
-#endif
   }
   static __device__ __forceinline__ f32x4 mix(f32x4 a, float wa, f32x4 b, float wb) {
-#ifdef FA_DIAG_FREE_CONTRACT
-    return a * wa + b * wb;
-#else
     return f32x4{mix(a[0], wa, b[0], wb), mix(a[1], wa, b[1], wb), mix(a[2], wa, b[2], wb),
                  mix(a[3], wa, b[3], wb)};
-#endif
   }
-  // KV-pair merge (attention_kvpair): the partner wave's state goes through LDS
-  // lane-linearly (both waves hold the same query rows in the same lanes).
-  // Region per wave: 2*NE f32x4 of O, then one f32x4 {m_0, l_0, m_1, l_1}.
-  static constexpr int MERGE_BYTES = (2 * NE + 1) * 64 * 16;
-  __device__ __forceinline__ void put_partial(char* region) const {
-    static_assert(QB == 2, "KV-pair merge layout: two query blocks per wave");
-    f32x4* d = reinterpret_cast<f32x4*>(region);
-#pragma unroll
-    for (int b = 0; b < QB; ++b)
-#pragma unroll
-      for (int e = 0; e < NE; ++e) d[(b * NE + e) * 64 + lane] = acc[b][e];
-    d[2 * NE * 64 + lane] = f32x4{m_ref[0], row_sum(0), m_ref[1], row_sum(1)};
-  }
-  // O = O_a 2^(m_a-M) + O_b 2^(m_b-M), l likewise, M = max over partials that saw a key
-  __device__ __forceinline__ void merge_partial(const char* region) {
-    static_assert(QB == 2, "KV-pair merge layout: two query blocks per wave");
-    const f32x4* d = reinterpret_cast<const f32x4*>(region);
-    const f32x4 ml = d[2 * NE * 64 + lane];
-#pragma unroll
-    for (int b = 0; b < QB; ++b) {
-      const float la = row_sum(b), lb = ml[2 * b + 1];
-      const float ma = la > 0.f ? m_ref[b] : ninf();
-      const float mb = lb > 0.f ? ml[2 * b] : ninf();
-      float M = fmaxf(ma, mb);
-      M = M == ninf() ? 0.f : M;
-      const float wa = __builtin_amdgcn_exp2f(ma - M), wb = __builtin_amdgcn_exp2f(mb - M);
-#pragma unroll
-      for (int e = 0; e < NE; ++e) acc[b][e] = mix(acc[b][e], wa, d[(b * NE + e) * 64 + lane], wb);
-      const float l = mix(la, wa, lb, wb);
-#ifdef FA_ROWSUM_VALU
-      lacc[b] = f32x4{g == 0 ? l : 0.f, 0.f, 0.f, 0.f};  // row_sum() adds the 4 lanes of a row
-#else
-      lacc[b] = f32x4{l, l, l, l};
-#endif
-      m_ref[b] = M;
-    }
-  }
-  // Symmetric KV-pair merge: group A finalizes row block 0 and parks block 1,
-  // group B the reverse.  Region per parked block: NE f32x4 of O, then one
-  // float2 {m, l} per lane.  The combine keeps group A's term first in both
-  // groups, so the result is bit-identical to merge_partial's.
+  // KV-pair merge (attention_kvpair), symmetric: group A finalizes row block
+  // 0 and parks block 1, group B the reverse (both waves of a SIMD hold the
+  // same query rows in the same lanes).  Region per parked block: NE f32x4 of
+  // O, then one float2 {m, l} per lane.  Both groups combine with group A's
+  // term first:  O = O_a 2^(m_a-M) + O_b 2^(m_b-M), l likewise, M = max over
+  // the partials that saw a key.
   static constexpr int HALF_MERGE_BYTES = NE * 64 * 16 + 64 * 8;
   template <int b>
   __device__ __forceinline__ void put_block(char* region) const {
@@ -1222,20 +612,16 @@ struct M16 {
       acc[b][e] = mix(oa, wa, ob, wb);
     }
     const float l = mix(la, wa, lb, wb);
-#ifdef FA_ROWSUM_VALU
-    lacc[b] = f32x4{g == 0 ? l : 0.f, 0.f, 0.f, 0.f};
-#else
     lacc[b] = f32x4{l, l, l, l};
-#endif
     m_ref[b] = M;
   }
   // Symmetric KV-quad merge: the four partials of a row set each finalize
   // one quarter -- partial P takes row block P & 1 and d-half P >> 1 -- and
   // park the three quarters the others finalize (slot (Q - P + 3) & 3 of
   // their region) plus {m_0, l_0, m_1, l_1}.  Each finalizer replays the
-  // sequential merge of the single-finalizer path (partial 0, then 1, 2, 3;
-  // the accumulated state is always the A side), so the result is
-  // bit-identical to it.
+  // sequential merge of a single finalizer (partial 0, then 1, 2, 3; the
+  // accumulated state is always the A side), so all four agree bit for bit
+  // with that order.
   static constexpr int QE = NE / 2;  // d-blocks per quarter
   static constexpr int QUARTER_BYTES = QE * 64 * 16;
   static constexpr int QUAD_MERGE_BYTES = 3 * QUARTER_BYTES + 64 * 16;
@@ -1301,11 +687,7 @@ struct M16 {
     }
 #pragma unroll
     for (int e = 0; e < QE; ++e) acc[b][e0 + e] = o[e];
-#ifdef FA_ROWSUM_VALU
-    lacc[b] = f32x4{g == 0 ? l : 0.f, 0.f, 0.f, 0.f};
-#else
     lacc[b] = f32x4{l, l, l, l};
-#endif
     m_ref[b] = m;
   }
   // m in the reference's units (scaled score, natural log): m_ref * ln 2
@@ -1326,7 +708,7 @@ struct M16 {
 
 // ---------------------------------------------------------------------------
 // The tile loop (shared skeleton)
-//   Pol    : M32<BN> or M16<BN>
+//   Pol    : M16<BN, T, HDIM>
 //   WAVES  : 64-lane waves per workgroup (BM = 32*WAVES query rows)
 //   CAUSAL : top-left aligned causal mask (key j visible to query i iff j <= i)
 //   SPLIT  : write unnormalised fp32 O + (m, l) instead of fp16 O
@@ -1336,7 +718,7 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
                                                     char* smem) {
   constexpr int BN = Pol::BN;
   constexpr int NT = WAVES * 64;
-  constexpr int RW = Pol::RW;              // query rows per wave (32, or 64 at one wave per SIMD)
+  constexpr int RW = Pol::RW;              // query rows per wave (32)
   constexpr int BM = WAVES * RW;
   constexpr int HD = Pol::HDIM;            // shadows the head_dim-128 defaults
   constexpr int ROW_BYTES = 2 * HD;        // HBM row
@@ -1432,9 +814,6 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
     char* kb_next = smem + (BUF ^ 1) * 2 * TILE_BYTES;
     const int kv0 = kv_lo + j * BN;
     FA_TSTAMP(sa);
-#ifdef FA_DIAG_W4_NO_STAGE  // timing-only bound (wrong results): no in-loop K/V staging at 64 rows/wave
-    if constexpr (RW != 64)
-#endif
     issue_loads(kv0 + BN);  // past kv_hi: zero bytes, no memory traffic
     FA_TSTAMP(sb);
     // wave-uniform: does any key of this tile lie at/below some row of this wave?
@@ -1443,9 +822,6 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
       pol.template tile<CAUSAL>(kb, kb + TILE_BYTES, kv0, kv_hi, qw, c, need_mask);
     }
     FA_TSTAMP(sc);
-#ifdef FA_DIAG_W4_NO_STAGE
-    if constexpr (RW != 64)
-#endif
     write_lds(kb_next);
     FA_TSTAMP(sd);
     __syncthreads();
@@ -1499,13 +875,10 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
 // DMA: K/V tiles go global -> LDS by LDS-DMA into three rotating buffers
 // (a tile's buffer must be free when its loads are issued, one half-step
 // before the register path would write it), no staging registers.
-// FA_PRIO_MODE (experiment): 0 = s_setprio 1 around every MFMA phase,
-// 1 = none, 2 = static: the younger half (waves 4-7) at priority 1 for the
-// whole loop (guide T5 static form), 3 = s_setprio 1 around every softmax
-// phase instead (the VALU side first)
-#ifndef FA_PRIO_MODE
-#define FA_PRIO_MODE 0
-#endif
+// Priority: the MFMA-phase wave runs at s_setprio 1 (every phase).  No
+// priority, the static young-half form (guide T5) and priority to the softmax
+// phase were each 1-6 % slower (profiles/r01_ab_priority_modes.jsonl,
+// r02_ab_priority_modes_d64.jsonl).
 template <class Pol, bool CAUSAL, bool SPLIT, bool PRIO = true, bool DMA = false>
 __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, int qb, int split,
                                                    char* smem) {
@@ -1546,12 +919,12 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   // phase is the shorter one (non-causal: +2 % at S=8192; causal: -5 %, its
   // masked/inactive tiles shorten the MFMA phases instead)
   constexpr bool kIssueInSm =
-      DMA || (!CAUSAL && (Pol::HDIM == 128 || FA_NC_D64_ISSUE_IN_SM));  // DMA: three buffers
+      DMA || (!CAUSAL && (Pol::HDIM == 128 || kNcD64IssueInSm));  // DMA: three buffers
   // where a tile is written to LDS: at the start of the softmax phase (beside
   // the partner's MFMAs; causal: +0.3-0.7 % A/B) or at its end (non-causal:
   // early was -0.8 %, its loads are issued in the softmax phase and need it
   // to land)
-  constexpr bool kWriteEarly = !DMA && (CAUSAL || (Pol::HDIM == 64 && FA_NC_D64_WRITE_EARLY));
+  constexpr bool kWriteEarly = !DMA && (CAUSAL || (Pol::HDIM == 64 && kNcD64WriteEarly));
   static_assert(!DMA || Pol::HDIM == 128, "LDS-DMA path: head_dim 128");
 
 #ifdef FA_STAMPS
@@ -1641,17 +1014,15 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   auto mfma_block = [&](int k) {
     // the MFMA-phase wave wins VALU/MFMA issue arbitration against its SIMD
     // partner (which is in its softmax phase), so its matrix stream stays dense
-    if constexpr (PRIO && FA_PRIO_MODE == 0) __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
     pol.mfma_block(kbuf(k), vbuf(k - 1), k >= 1 && active(k - 1), k < n && active(k));
-    if constexpr (PRIO && FA_PRIO_MODE == 0) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   };
   auto softmax_block = [&](int k) {
     if (k < n && active(k)) {
       const int kv0 = kv_lo + k * BN;
       const bool need_mask = (kv0 + BN > kv_hi) || (CAUSAL && kv0 + BN - 1 > qw);
-      if constexpr (PRIO && FA_PRIO_MODE == 3) __builtin_amdgcn_s_setprio(1);
       pol.template softmax<CAUSAL>(kv0, kv_hi, qw, c, need_mask);
-      if constexpr (PRIO && FA_PRIO_MODE == 3) __builtin_amdgcn_s_setprio(0);
     }
   };
 
@@ -1659,9 +1030,6 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   // executes one extra barrier first (while A runs MFMA_0) and A one extra at
   // the end, so B trails A by exactly one half-step with no group-specific
   // code path.  Tile t = k + grp is loaded during MFMA_k and written during SM_k.
-  if constexpr (PRIO && FA_PRIO_MODE == 2) {
-    if (grp == 1) __builtin_amdgcn_s_setprio(1);
-  }
   if (grp == 1) {
     if (n > 0) write_tile(0);
     if (kIssueInSm && 1 < n) issue_tile(1);
@@ -1688,13 +1056,9 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   // keep the LDS hand-off order for the next item.  Causal only: +1-3 % on
   // the causal persistent shapes, while the non-causal build took more SGPR
   // spills (35 -> 42) and was level to 4 % slower
-  // (profiles/r02_ab_early_o_store.jsonl).  FA_LATE_STORE: the round-1 order
-  // (both groups store after the final barrier).
-#ifdef FA_LATE_STORE
-  constexpr bool kEarlyStore = false;
-#else
-  constexpr bool kEarlyStore = CAUSAL || (Pol::HDIM == 64 && FA_NC_D64_EARLY_STORE);
-#endif
+  // (profiles/r02_ab_early_o_store.jsonl).  Non-causal d128: both groups
+  // store after the final barrier.
+  constexpr bool kEarlyStore = CAUSAL || (Pol::HDIM == 64 && kNcD64EarlyStore);
   auto store_out = [&]() {
     if constexpr (!SPLIT) {
       pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);
@@ -1754,7 +1118,6 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
     __syncthreads();
   }
   if (grp == 0) __syncthreads();
-  if constexpr (PRIO && FA_PRIO_MODE == 2) __builtin_amdgcn_s_setprio(0);
 #ifdef FA_STAMPS
   const unsigned long long t_le = __builtin_amdgcn_s_memtime();
 #endif
@@ -1801,30 +1164,15 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
 // that leave CUs idle even at 128 rows (B=1 H=32 S=512: 128 KV-pair
 // workgroups on 256 CUs).  One staging set (loads one half-step ahead): two
 // sets of the double-width stage would not fit the 256 VGPRs.
-// KV-pair merge: 1 = symmetric (each group parks one 16-row block and
-// finalizes and stores the other, so all eight waves share the merge and the
-// O stores; bit-identical, level to +1.4 % on the KV-pair shapes,
-// profiles/r02_ab_kvpair_sym_merge.jsonl), 0 = group A merges both blocks
-// and stores all 128 rows (round 1)
-#ifndef FA_KVPAIR_SYM_MERGE
-#define FA_KVPAIR_SYM_MERGE 1
-#endif
-// Short-tier Q: 1 = each Q chunk read once per workgroup and shared through
-// LDS by the row set's partial waves (bit-identical; KV-quad +3.5-12.6 %,
-// profiles/r02_ab_short_q_share.jsonl), 0 = every wave loads its own Q
-#ifndef FA_KVQUAD_SHARE_Q
-#define FA_KVQUAD_SHARE_Q 1
-#endif
-// KV-quad merge (A/B knob): 1 = symmetric (each of the four partials of a
-// row set finalizes and stores a quarter), 0 = partial 0 merges all
-#ifndef FA_KVQUAD_SYM_MERGE
-#define FA_KVQUAD_SYM_MERGE 1
-#endif
-// KV-pair / KV-quad priority (A/B knob): 1 = s_setprio 1 around every MFMA
-// half-step (default), 0 = none, 2 = around every softmax half-step instead
-#ifndef FA_KVPAIR_PRIO
-#define FA_KVPAIR_PRIO 1
-#endif
+// Merges are symmetric: in the KV-pair each group parks one 16-row block and
+// finalizes and stores the other, in the KV-quad each of a row set's four
+// partials finalizes and stores a quarter, so all eight waves share the merge
+// and the O stores (bit-identical to one finalizer; +1-7 %,
+// profiles/r02_ab_kvpair_sym_merge.jsonl, r02_ab_merge_contraction.jsonl).
+// Q is read once per workgroup and shared through LDS by the row set's
+// partial waves (bit-identical; KV-quad +3.5-12.6 %,
+// profiles/r02_ab_short_q_share.jsonl).  The MFMA half-step runs at
+// s_setprio 1.
 template <class Pol, bool CAUSAL, int SUB = 1>
 __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int qb, char* smem) {
   static_assert(SUB == 1 || SUB == 2, "key split 2 (KV-pair) or 4 (KV-quad)");
@@ -1843,8 +1191,6 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   constexpr bool TWO_SETS = SUB == 1;
   constexpr int NSET = TWO_SETS ? 2 : 1;
   static_assert((SBN * (HD / 8)) % NT == 0, "tile chunks must divide evenly");
-  static_assert((NP - 1) * RW * Pol::MERGE_BYTES <= (SUB == 1 ? kKvpairLdsBytes : kKvquadLdsBytes),
-                "merge region fits the LDS allocation");
   static_assert(4 * STAGE_BYTES <= (SUB == 1 ? kKvpairLdsBytes : kKvquadLdsBytes),
                 "stage buffers fit the LDS allocation");
 
@@ -1888,16 +1234,11 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   // the partials of a row set share one read of its Q through LDS: KV-quad
   // through the stage-0 V buffer (first written after a later barrier),
   // KV-pair past the four tile buffers (its stage-0 V buffer is too small)
-  constexpr bool kShareQ = SUB == 2 ? FA_KVQUAD_SHARE_Q : FA_KVPAIR_SHARE_Q;
   char* qshare = smem + (SUB == 2 ? 2 : 4) * STAGE_BYTES + rw * Pol::Q_SHARE_BYTES;
-  static_assert(!kShareQ || SUB == 1 || RW * Pol::Q_SHARE_BYTES <= STAGE_BYTES,
-                "Q share fits one V buffer");
-  static_assert(!kShareQ || SUB == 2 || 4 * STAGE_BYTES + RW * Pol::Q_SHARE_BYTES <= kKvpairLdsBytes,
+  static_assert(SUB == 1 || RW * Pol::Q_SHARE_BYTES <= STAGE_BYTES, "Q share fits one V buffer");
+  static_assert(SUB == 2 || 4 * STAGE_BYTES + RW * Pol::Q_SHARE_BYTES <= kKvpairLdsBytes,
                 "Q share fits past the tile buffers");
-  if constexpr (kShareQ)
-    pol.template issue_q_part<NP>(make_rsrc(Qh, S * ROW_BYTES), qw, pidx);
-  else
-    pol.issue_q(make_rsrc(Qh, S * ROW_BYTES), qw);
+  pol.template issue_q_part<NP>(make_rsrc(Qh, S * ROW_BYTES), qw, pidx);
 
   auto kbuf = [&](int x) { return smem + (x & 1) * STAGE_BYTES; };
   auto vbuf = [&](int x) { return smem + (2 + (x & 1)) * STAGE_BYTES; };
@@ -1959,10 +1300,7 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
       issue_stage(0, Set0{});
     }
     __builtin_amdgcn_sched_barrier(0);  // all prologue loads issued first (attention_tile_loop)
-    if constexpr (kShareQ)
-      pol.template scale_put_q_part<NP>(qshare, pidx);
-    else
-      pol.scale_q();
+    pol.template scale_put_q_part<NP>(qshare, pidx);
 #pragma unroll
     for (int i = 0; i < NCH; ++i)
       *reinterpret_cast<f16x8*>(kbuf(0) + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = k0[i];
@@ -1970,7 +1308,7 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   // Q and K_0 retired (see attention_tile_loop); the stage loads may stay in flight
   __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * NSET * NCH));
   __syncthreads();
-  if constexpr (kShareQ) pol.template get_q_rest<NP>(qshare, pidx);
+  pol.template get_q_rest<NP>(qshare, pidx);
 #ifdef FA_STAMPS
   st_acc[7] = __builtin_amdgcn_s_memtime() - t_in;
 #endif
@@ -2010,10 +1348,10 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   for (int m = 0; m < P; ++m) {
     const int h = 2 * m + grp;
     FA_KSTAMP(sa);
-    if constexpr (FA_KVPAIR_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
     pol.mfma_block(kbuf(h) + sub * TILE_BYTES, vbuf(h - 2) + sub * TILE_BYTES, active(h - 2),
                    active(h));
-    if constexpr (FA_KVPAIR_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
     FA_KSTAMP(sb);
 #ifdef FA_STAMPS
     st_acc[0] += sb - sa;
@@ -2023,9 +1361,7 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
     if (active(h)) {
       const int kv0 = (SUB * h + sub) * BN;
       const bool need_mask = (kv0 + BN > kv_hi) || (CAUSAL && kv0 + BN - 1 > qw);
-      if constexpr (FA_KVPAIR_PRIO == 2) __builtin_amdgcn_s_setprio(1);
       pol.template softmax<CAUSAL>(kv0, kv_hi, qw, c, need_mask);
-      if constexpr (FA_KVPAIR_PRIO == 2) __builtin_amdgcn_s_setprio(0);
     }
     FA_KSTAMP(sb);
 #ifdef FA_STAMPS
@@ -2040,12 +1376,9 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   const unsigned long long t_le = __builtin_amdgcn_s_memtime();
 #endif
 
-  // merge: group B parks its partial state, group A combines and stores
-  // (FA_DIAG_NO_MERGE: diagnostic timing build only, group A stores its half
-  // unmerged -- the merge costs 2-7 % at B=1 H=32 S=512-2048)
-#if FA_KVQUAD_SYM_MERGE && !defined(FA_DIAG_NO_MERGE)
+  // merge (symmetric, see above)
   if constexpr (SUB == 2) {
-    // symmetric: each of a row set's four partials finalizes one quarter
+    // each of a row set's four partials finalizes one quarter
     static_assert(NP * RW * Pol::QUAD_MERGE_BYTES <= kKvquadLdsBytes, "quarter-merge region fits");
     const int stride = RW * Pol::QUAD_MERGE_BYTES;
     char* regions = smem + rw * Pol::QUAD_MERGE_BYTES;  // partial j at regions + j * stride
@@ -2066,13 +1399,8 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
       pol.template merge_quarter<3>(regions, stride);
       pol.template store_o<1, 2, H, 2 * H>(ro, qw);
     }
-    return;
-  }
-#endif
-#if FA_KVPAIR_SYM_MERGE && !defined(FA_DIAG_NO_MERGE)
-  if constexpr (SUB == 1) {
-    // symmetric: each group parks one row block and finalizes the other, so
-    // the merge and the O stores are split over all eight waves
+  } else {
+    // each group parks one row block and finalizes the other
     static_assert(2 * RW * Pol::HALF_MERGE_BYTES <= kKvpairLdsBytes, "half-merge region fits");
     if (grp == 0)
       pol.template put_block<1>(smem + rw * Pol::HALF_MERGE_BYTES);
@@ -2087,187 +1415,15 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
       pol.template merge_block<1, false>(smem + rw * Pol::HALF_MERGE_BYTES);
       pol.template store_o<1, 2>(ro, qw);
     }
-    return;
-  }
-#endif
-#ifndef FA_DIAG_NO_MERGE
-  // partial j >= 1 of row wave rw parks in slot (j - 1) RW + rw
-  if (pidx > 0) pol.put_partial(smem + ((pidx - 1) * RW + rw) * Pol::MERGE_BYTES);
-  __syncthreads();
-#endif
-#ifdef FA_STAMPS
-  unsigned long long e1, e2;
-  FA_KSTAMP(e1);
-#endif
-  if (pidx == 0) {
-#ifndef FA_DIAG_NO_MERGE
-#pragma unroll
-    for (int j = 1; j < NP; ++j) pol.merge_partial(smem + ((j - 1) * RW + rw) * Pol::MERGE_BYTES);
-#endif
-    pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);
   }
 #ifdef FA_STAMPS
-  FA_KSTAMP(e2);
-  st_acc[5] = (e1 - t_le) * st_acc[6];   // printed per iteration: park + barrier
-  st_acc[11] = e2 - e1;                  // merge + store issue
   __builtin_amdgcn_s_waitcnt(0);
-  st_acc[8] = __builtin_amdgcn_s_memtime() - t_le;
+  st_acc[8] = __builtin_amdgcn_s_memtime() - t_le;  // merge + stores retired
   st_acc[9] = 1;
   if (lane == 0 && blockIdx.x < 64)
     for (int i = 0; i < 12; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
 #endif
 #undef FA_KSTAMP
 }
-
-#ifdef FA_W4_EXPERIMENT  // tools/experiments/w4_spill_probe.sh (not in the library)
-// ---------------------------------------------------------------------------
-// W4 skeleton: 4 waves (one per SIMD), 64 query rows per wave, 256 rows per
-// workgroup.  Against the 8-wave ping-pong (32 rows per wave) every K/V
-// fragment read from LDS now feeds four MFMAs instead of two: half the LDS
-// bytes per FLOP, the ping-pong's measured largest non-MFMA cost.  With no
-// SIMD partner to hide the softmax behind, the wave overlaps it with its own
-// MFMAs by software pipelining across key tiles (iteration j):
-//   block 1: PV(j-1) first half      beside  row maxima of S(j)
-//   (rare, wave-uniform) move m_ref, shift S(j)
-//   block 2: PV(j-1) second half,    beside  P(j) = exp2(S(j)), cvt to fp16,
-//            QK^T(j+1)                        stage writes / next loads
-//   (rare) O, l *= alpha
-//   barrier
-// S(j+1) reuses the S(j) registers: the compiler orders each cvt before the
-// QK^T MFMA that overwrites its source.  O and l take alpha after PV(j-1)
-// because P(j-1) was relative to the old m_ref.
-// LDS: K and V double-buffered; stage j = (K_{j+2}, V_j) is loaded in
-// iteration j-1 (register staged) and written in iteration j.  K_{j+1} is
-// read in iteration j, V_{j-1} too, and each buffer written in iteration j
-// was last read in iteration j-1: one barrier per tile.
-// Causal: every tile up to the workgroup's diagonal runs on every wave (the
-// last wave needs them all and the barrier makes the others wait anyway);
-// tiles past a wave's rows are masked to -inf and contribute exp2 = 0.
-// ---------------------------------------------------------------------------
-template <class Pol, bool CAUSAL>
-__device__ __forceinline__ void attention_w4(const FwdParams& p, int bh, int qb, char* smem) {
-  constexpr int WAVES = 4;
-  constexpr int BN = Pol::BN;
-  constexpr int NT = WAVES * 64;
-  constexpr int RW = 16 * Pol::QB;           // query rows per wave
-  constexpr int BM = WAVES * RW;
-  constexpr int HD = Pol::HDIM;
-  constexpr int ROW_BYTES = 2 * HD;
-  constexpr int TILE_BYTES = BN * 256;
-  constexpr int NCH = (BN * (HD / 8)) / NT;  // 16-B chunks per thread per tile (K and V each)
-  static_assert((BN * (HD / 8)) % NT == 0, "tile chunks must divide evenly");
-  static_assert(Pol::QB == 4, "W4: 64 query rows per wave");
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int S = p.seq_len;
-
-  const size_t head_off = (size_t)bh * (size_t)S * HD;
-  const f16* Qh = p.q + head_off;
-  const f16* Kh = p.k + head_off;
-  const f16* Vh = p.v + head_off;
-
-  const int q0 = qb * BM;
-  const int qw = q0 + wave * RW;
-  const int kv_hi = CAUSAL ? min(q0 + BM, S) : S;
-  const int n = (kv_hi + BN - 1) / BN;
-
-  Pol pol;
-  pol.init(lane, p.c);
-  pol.issue_q(make_rsrc(Qh, S * ROW_BYTES), qw);
-
-  auto kbuf = [&](int x) { return smem + (x & 1) * TILE_BYTES; };
-  auto vbuf = [&](int x) { return smem + (2 + (x & 1)) * TILE_BYTES; };
-  const int kr0 = pol.k_stage_row(wave), kc = pol.k_stage_ch();
-  const int vr0 = pol.v_stage_row(wave), vc = pol.v_stage_ch();
-  f16x8 kst[NCH], vst[NCH];
-  // stage j = (K_{j+2}, V_j); rows at/after kv_hi and tiles < 0 read as 0
-  auto issue_stage = [&](int j) {
-    const int kb_row = (j + 2) * BN, vb_row = j * BN;
-    const auto rk = make_rsrc(Kh + (size_t)min(kb_row, S) * HD, (kv_hi - kb_row) * ROW_BYTES);
-    const auto rv = make_rsrc(Vh + (size_t)max(vb_row, 0) * HD,
-                              vb_row < 0 ? 0 : (kv_hi - vb_row) * ROW_BYTES);
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      kst[i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
-      vst[i] = buf_load16(rv, (vr0 + Pol::RPW * WAVES * i) * ROW_BYTES + vc * 16);
-    }
-  };
-  auto write_stage = [&](int j) {
-    char* kb = kbuf(j + 2);
-    char* vb = vbuf(j);
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      *reinterpret_cast<f16x8*>(kb + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = kst[i];
-      *reinterpret_cast<f16x8*>(vb + Pol::v_lds(vr0 + Pol::RPW * WAVES * i, vc)) = vst[i];
-    }
-  };
-
-  // prologue: Q, K_0 and stage -1 (K_1) in flight together
-  {
-    const auto rk = make_rsrc(Kh, kv_hi * ROW_BYTES);
-    f16x8 k0[NCH];
-#pragma unroll
-    for (int i = 0; i < NCH; ++i)
-      k0[i] = buf_load16(rk, (kr0 + Pol::RPW * WAVES * i) * ROW_BYTES + kc * 16);
-    issue_stage(-1);
-    __builtin_amdgcn_sched_barrier(0);  // all prologue loads issued first (attention_tile_loop)
-    pol.scale_q();
-#pragma unroll
-    for (int i = 0; i < NCH; ++i)
-      *reinterpret_cast<f16x8*>(kbuf(0) + Pol::k_lds(kr0 + Pol::RPW * WAVES * i, kc)) = k0[i];
-  }
-  __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * NCH));  // Q, K_0 retired; stage -1 may fly
-  __syncthreads();
-
-  // iteration -1: QK^T(0), stage -1 written, stage 0 loads issued
-  write_stage(-1);
-  issue_stage(0);
-  pol.qk(kbuf(0));
-  __syncthreads();
-
-  // one pipelined iteration (j = the softmax tile), P buffer PB = j & 1:
-  //   PV(j-1) beside exp/cvt of S(j); O, l *= alpha(j) after PV(j-1) (rare);
-  //   then QK^T(j+1) chain-major beside the stage traffic, and the row
-  //   maxima / rare rescale bookkeeping of S(j+1).  One body per P buffer;
-  //   the mask is a runtime branch around the masking code only.
-  auto need_mask = [&](int j) {
-    const int kv0 = j * BN;
-    return (kv0 + BN > kv_hi) || (CAUSAL && kv0 + BN - 1 > qw);
-  };
-  bool resc = false;
-  auto iter = [&](int j, auto pb_c) {
-    constexpr int PB = decltype(pb_c)::value;
-    if (j >= 1) pol.template pv_buf<PB ^ 1>(vbuf(j - 1));
-    pol.template exp_cvt<PB>();
-    if (resc) pol.sm_alpha();  // alpha(j): O holds PV(..j-1) at the old m_ref
-    resc = false;
-    if (j + 1 < n) pol.qk_cm(kbuf(j + 1));
-    write_stage(j);
-    issue_stage(j + 1);
-    if (j + 1 < n) {
-      if (pol.template sm_max<CAUSAL>((j + 1) * BN, kv_hi, qw, need_mask(j + 1))) resc = pol.sm_shift();
-    }
-    __syncthreads();
-  };
-  using P0 = std::integral_constant<int, 0>;
-  using P1 = std::integral_constant<int, 1>;
-  // S(0): row maxima and first m_ref (the first shift only centres m_ref: O is zero)
-  if (n > 0 && pol.template sm_max<CAUSAL>(0, kv_hi, qw, need_mask(0))) pol.sm_shift();
-  int j = 0;
-  for (; j + 1 < n; j += 2) {
-    iter(j, P0{});
-    iter(j + 1, P1{});
-  }
-  if (j < n) {
-    iter(j, P0{});
-    pol.template pv_buf<0>(vbuf(j));
-  } else if (n > 0) {
-    pol.template pv_buf<1>(vbuf(j - 1));
-  }
-  pol.store_o(make_rsrc(p.o + head_off, S * ROW_BYTES), qw);
-}
-#endif  // FA_W4_EXPERIMENT
 
 }  // namespace fa

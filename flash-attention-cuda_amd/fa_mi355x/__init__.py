@@ -291,6 +291,12 @@ def flash_attention_fwd_splitkv(q, k, v, causal: bool = False, num_splits: int =
     """Split-KV forward + log-sum-exp merge (ref split-K path, :169-180/:559-598)."""
     import torch
 
+    # the split-KV entry is fp16-only (fa_fwd_f16_splitkv takes untyped
+    # pointers, as the reference's half* split-K path does, :606-611): a bf16
+    # tensor would be read as fp16 bits, so reject it before anything else
+    if q.dtype != torch.float16:
+        raise FlashAttentionError(FA_ERR_BAD_SHAPE,
+                                  f"split-KV takes float16 tensors only, got {q.dtype}")
     if out is None:
         out = torch.empty_like(q)
     _check_qkvo(q, k, v, out)
@@ -330,6 +336,15 @@ def flash_attention_v9_dispatch(Q, K, V, Output, splitk_buf_O, splitk_buf_ml, ba
     Raises FlashAttentionError where the reference would exit(EXIT_FAILURE).
     """
     del splitk_buf_O, splitk_buf_ml
+
+    # the reference's boundary is typed half* (:606-611): tensors must be
+    # float16 (raw pointers cannot be checked and are taken as fp16 BHSD)
+    for name, x in (("Q", Q), ("K", K), ("V", V), ("Output", Output)):
+        if not isinstance(x, int):
+            import torch
+
+            if x.dtype != torch.float16:
+                raise FlashAttentionError(FA_ERR_BAD_SHAPE, f"{name} must be float16, got {x.dtype}")
 
     def ptr(x):
         return x if isinstance(x, int) else x.data_ptr()

@@ -1,5 +1,5 @@
 """Interleaved A/B timing of tile configs in ONE process (guide §5.4 rule 24).
-usage: python tools/ab.py --configs 8,10 --seq 8192 [--causal] [--batch B] [--heads H]
+usage: python tools/ab.py --configs 2,6 --seq 8192 [--causal] [--batch B] [--heads H]
        [--rounds 7] [--iters 30]
 Prints per-config median / min TFLOPS over rounds (random uniform[-0.5,0.5] fp16)."""
 import argparse

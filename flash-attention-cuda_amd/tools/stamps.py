@@ -1,5 +1,5 @@
 """Phase-stamp diagnostic (loads lib/libfa_mi355x_stamps.so, NOT the product lib).
-usage: python tools/stamps.py --config 8 --seq 8192 [--causal] [--batch B]
+usage: python tools/stamps.py --config 6 --seq 8192 [--causal] [--batch B]
 Prints per-wave mean cycles per loop iteration in: MFMA block, barrier-1, softmax block, barrier-2."""
 import argparse
 import ctypes

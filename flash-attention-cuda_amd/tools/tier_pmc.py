@@ -18,6 +18,12 @@ Derived per launch (first launch of each shape dropped):
                 -- fraction of SIMD-cycles the matrix pipe was busy, at whatever
                 clock the chip held (the guide's DVFS note)
   eff_clock   = GRBM_GUI_ACTIVE / 8 / profiled kernel time
+  tflops_prof = algorithmic FLOPs / profiled kernel time (the SAME dispatches
+                the counters come from; profiled runs hold a lower clock, so
+                this is below the un-profiled HIP-event TFLOP/s)
+  identity    = mfma_busy x eff_clock x 1024 SIMDs x 1024 FLOP/clk
+                / (MFMA FLOPs issued per useful FLOP) / tflops_prof -- 1.00
+                when busy cycles, clock and time all come from one run
   frac_nominal = TFLOP/s (un-profiled, HIP events) / 2516.6
   hbm_gbs     = (FETCH + WRITE bytes) / un-profiled time
 """
@@ -40,10 +46,7 @@ SHAPES = [  # (label, batch, heads, seq, causal)
     ("headline_b64_s4096_causal", 64, 32, 4096, True),
     ("s256_b16_noncausal", 16, 32, 256, False),
     # non-dispatched tile configs (BM, BN, waves) on the same shapes: the
-    # 64-rows-per-wave W4x64 tiers and the per-item 8-wave ping-pong
-    ("w4x64_s8192_noncausal", 1, 32, 8192, False, "bm256_bn64_w4x64_m16_persistent_noncausal"),
-    ("w4x64_s8192_causal", 1, 32, 8192, True, "bm256_bn64_w4x64_m16_persistent_causal"),
-    ("w4x64_headline_b64_s4096_causal", 64, 32, 4096, True, "bm256_bn64_w4x64_m16_persistent_causal"),
+    # per-item 8-wave ping-pong (what the persistent order buys)
     ("pingpong_item_s8192_causal", 1, 32, 8192, True, "bm256_bn64_w8_m16_pingpong_causal"),
 ]
 ITERS = 6
@@ -128,14 +131,21 @@ def summary(timing_jsonl, mfma_dir, fetch_dir, write_dir, out):
         busy, grbm, nmf = mean(m["SQ_VALU_MFMA_BUSY_CYCLES"]), mean(m["GRBM_GUI_ACTIVE"]), mean(m["SQ_INSTS_MFMA"])
         hbm = mean(f["FETCH_SIZE"]) * 1024 * 2 + mean(w["WRITE_SIZE"]) * 1024
         t = timing[label]
+        mfma_per_flop = nmf * 16384.0 / t["flops"]  # 16x16x32: 16384 FLOP per MFMA
+        busy_frac = busy / (SIMDS * grbm / XCDS)
+        ghz = grbm / XCDS / mean(dur)
+        tf_prof = t["flops"] / (mean(dur) * 1e-9) / 1e12
         rows.append({
             "label": label, "config": t["config"], "kernel": kn[i * ITERS].split("(")[0],
             "batch": b, "heads": h, "seq": s, "causal": causal,
             "ms": round(t["ms"], 4), "tflops": round(t["tflops"], 1),
             "frac_nominal_peak": round(t["tflops"] / PEAK, 4),
-            "mfma_busy": round(busy / (SIMDS * grbm / XCDS), 4),
+            "mfma_busy": round(busy_frac, 4),
             "mfma_insts": nmf, "busy_cycles_per_mfma": round(busy / nmf, 2),
-            "eff_clock_ghz_profiled": round(grbm / XCDS / mean(dur), 3),
+            "mfma_per_useful_flop": round(mfma_per_flop, 4),
+            "eff_clock_ghz_profiled": round(ghz, 3),
+            "ms_profiled": round(mean(dur) / 1e6, 4), "tflops_profiled": round(tf_prof, 1),
+            "identity": round(busy_frac * ghz * SIMDS * 1024 / mfma_per_flop / 1e3 / tf_prof, 3),
             "hbm_bytes": int(hbm), "alg_bytes": int(t["alg_bytes"]),
             "traffic_over_alg": round(hbm / t["alg_bytes"], 3),
             "hbm_gbs": round(hbm / (t["ms"] / 1e3) / 1e9, 1),
@@ -144,11 +154,13 @@ def summary(timing_jsonl, mfma_dir, fetch_dir, write_dir, out):
     with open(out, "w") as fo:
         for r in rows:
             fo.write(json.dumps(r) + "\n")
-    hdr = f"{'shape':30s} {'tier':50s} {'TF/s':>7s} {'%peak':>6s} {'mfma':>6s} {'GHz':>5s} {'GB/s':>7s} {'tr/alg':>6s}"
+    hdr = (f"{'shape':30s} {'tier':50s} {'TF/s':>7s} {'%peak':>6s} | {'TF/s pr':>7s} {'mfma':>6s} "
+           f"{'GHz pr':>6s} {'ident':>5s} | {'GB/s':>7s} {'tr/alg':>6s}")
     print(hdr)
     for r in rows:
-        print(f"{r['label']:30s} {r['config']:50s} {r['tflops']:7.1f} {100*r['frac_nominal_peak']:6.1f} "
-              f"{100*r['mfma_busy']:6.1f} {r['eff_clock_ghz_profiled']:5.2f} {r['hbm_gbs']:7.1f} {r['traffic_over_alg']:6.2f}")
+        print(f"{r['label']:30s} {r['config']:50s} {r['tflops']:7.1f} {100*r['frac_nominal_peak']:6.1f} | "
+              f"{r['tflops_profiled']:7.1f} {100*r['mfma_busy']:6.1f} {r['eff_clock_ghz_profiled']:6.2f} "
+              f"{r['identity']:5.2f} | {r['hbm_gbs']:7.1f} {r['traffic_over_alg']:6.2f}")
 
 
 if __name__ == "__main__":

@@ -1,5 +1,5 @@
 """Workgroup timeline diagnostic (stamps build): per-CU busy fraction, tail, order.
-usage: python tools/timeline.py --config 9 --seq 8192 --causal [--batch B]"""
+usage: python tools/timeline.py --config 7 --seq 8192 --causal [--batch B]"""
 import argparse
 import collections
 import ctypes

@@ -3,7 +3,7 @@
 per counter as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE x1024 x2 +
 WRITE_SIZE x1024 per launch, first dispatch dropped).
 
-usage: python tools/traffic_ab.py --libs ,snake --config 15 --shapes 1x32x8192,1x32x16384 --causal
+usage: python tools/traffic_ab.py --libs ,snake --config 7 --shapes 1x32x8192,1x32x16384 --causal
 Prints one JSON line per (lib, shape): bytes per launch and the ratio to the
 algorithmic bytes 8*B*H*S*D (Q, K, V read once, O written once)."""
 import argparse

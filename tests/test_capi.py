@@ -201,6 +201,51 @@ def test_python_mirror_rejects_bad_tensors():
         fa.flash_attention_fwd(y, y, y)
 
 
+def test_fp16_only_entries_reject_bf16():
+    """The split-KV entry and the reference-signature mirror are fp16-only
+    (the reference's half* boundary, flash_attention.cu:606-611): bf16 tensors
+    raise before any pointer reaches the library (checked without a GPU)."""
+    torch = pytest.importorskip("torch")
+    fa = _fa()
+    x = torch.zeros(1, 1, 8, 128, dtype=torch.bfloat16)
+    with pytest.raises(fa.FlashAttentionError, match="float16"):
+        fa.flash_attention_fwd_splitkv(x, x, x, causal=False)
+    with pytest.raises(fa.FlashAttentionError, match="float16"):
+        fa.flash_attention_v9_dispatch(x, x, x, x, None, None, 1, 1, 8, 128, False)
+    y = torch.zeros(1, 1, 8, 128, dtype=torch.float32)
+    with pytest.raises(fa.FlashAttentionError, match="float16"):
+        fa.flash_attention_v9_dispatch(y, y, y, y, None, None, 1, 1, 8, 128, True)
+
+
+TWIN_PREFIXES = ("", "bf16_", "d64_", "bf16_d64_")
+
+
+def test_config_table_ships_only_used_tiers():
+    """Every shipped config is a tier the dispatcher picks (or a dtype /
+    head_dim twin of one), the explicit split-KV entry, or a baseline a test
+    compares against -- no dead experiments in the library."""
+    fa = _fa()
+    cfgs = fa.configs()
+    by_name = {c.name: c for c in cfgs}
+    used = set()
+    for causal in (False, True):
+        for s in (1, 64, 128, 200, 256, 300, 512, 768, 1024, 2048, 4096, 8192, 16384, 32768):
+            for b, h in ((1, 1), (1, 2), (1, 4), (1, 8), (1, 16), (1, 32), (1, 64), (2, 32),
+                         (4, 32), (8, 32), (16, 32), (64, 32), (3, 40), (1, 203)):
+                base = cfgs[fa.select_config(b, h, s, causal)].name
+                used |= {pre + base for pre in TWIN_PREFIXES if pre + base in by_name}
+    baselines = {"bm256_bn64_w8_m16_pingpong_noncausal", "bm256_bn64_w8_m16_pingpong_causal",
+                 "bm256_bn64_w8_m16_pingpong_persistent_dma_noncausal",
+                 "bm256_bn64_w8_m16_pingpong_persistent_dma_causal"}
+    explicit = {c.name for c in cfgs if c.split_kv}
+    unused = sorted(set(by_name) - used - baselines - explicit)
+    assert not unused, unused
+    # every dispatched fp16 d128 tier has all three twins
+    for name in used:
+        if not name.startswith(("bf16_", "d64_")):
+            assert all(pre + name in by_name for pre in TWIN_PREFIXES), name
+
+
 def test_bf16_configs_and_entry_points():
     """bf16 twins exist for the dispatched tiers; each entry point accepts
     only its own dtype's configs (checked before any launch: no GPU needed)."""

@@ -103,6 +103,29 @@ def test_long_causal_few_heads_kvquad(b, h, s):
             assert d <= TOL, f"b={bi} h={hi}: max_diff={d}"
 
 
+@pytest.mark.parametrize("dtype,head_dim", [("bfloat16", 128), ("float16", 64), ("bfloat16", 64)])
+@pytest.mark.parametrize("b,h,s", [(1, 4, 8192), (1, 8, 4096)])
+def test_long_causal_few_heads_kvquad_twins(b, h, s, dtype, head_dim):
+    # the same selector path through the bf16 / head_dim-64 twins (no oracle
+    # covers them): sampled query rows of every head against an fp32 torch
+    # reference of those rows, bf16 at the 5e-3 gate of tests/test_bf16_gpu.py
+    fa = _fa()
+    tdt = torch.float16 if dtype == "float16" else torch.bfloat16
+    shape = (b, h, s, head_dim)
+    q, k, v = (_rand(shape, 41 + i).to(tdt) for i in range(3))
+    o = fa.flash_attention_fwd(q, k, v, causal=True)
+    torch.cuda.synchronize()
+    rows = torch.tensor(_sample_rows(s, n=12), device=q.device)
+    qs = q[:, :, rows].float()
+    sc = qs @ k.float().transpose(-1, -2) / head_dim ** 0.5
+    keep = torch.arange(s, device=q.device)[None, :] <= rows[:, None]
+    sc = sc.masked_fill(~keep, float("-inf"))
+    ref = (torch.softmax(sc, dim=-1) @ v.float())
+    tol = TOL if dtype == "float16" else 5e-3
+    err = (o[:, :, rows].float() - ref).abs().max().item()
+    assert err <= tol, f"{dtype} d{head_dim}: max err {err}"
+
+
 @pytest.mark.parametrize("b,h,s,causal", [(2048, 32, 33, True), (512, 64, 200, False),
                                            (512, 64, 200, True)])
 def test_many_heads_sampled(b, h, s, causal):

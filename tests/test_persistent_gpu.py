@@ -5,7 +5,7 @@ sequence lengths, head counts that are not a multiple of the 8 XCD groups,
 and single-tile items.
 
 It runs exactly the per-tile arithmetic of the one-workgroup-per-item
-ping-pong kernel (configs 8/9) in the same order, so its output must be
+ping-pong kernel (bm256_bn64_w8_m16_pingpong_*) in the same order, so its output must be
 bit-identical to it; sampled heads are also checked against the oracle
 (reference cpu_attention restatement) at the 1e-3 gate.
 """
@@ -36,6 +36,14 @@ def _rand(shape, seed):
 
 def _bits(t):
     return t.detach().cpu().contiguous().view(torch.int16).numpy().view(np.uint16)
+
+
+def _base_ids():
+    """the per-item 8-wave ping-pong (the bit-identity baseline)"""
+    out = {c.causal: c.id for c in _fa().configs()
+           if c.name in ("bm256_bn64_w8_m16_pingpong_noncausal", "bm256_bn64_w8_m16_pingpong_causal")}
+    assert set(out) == {False, True}
+    return out
 
 
 def _ids(kind_name):
@@ -86,8 +94,7 @@ def test_persistent_bit_identical(kind, shape, causal):
     fa = _fa()
     b, h, s = shape
     q, k, v = (_rand((b, h, s, 128), 100 + i) for i in range(3))
-    base_id = 9 if causal else 8
-    out_base = fa.flash_attention_fwd(q, k, v, causal=causal, config=base_id)
+    out_base = fa.flash_attention_fwd(q, k, v, causal=causal, config=_base_ids()[causal])
     out = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(kind)[causal])
     torch.cuda.synchronize()
     cus = torch.cuda.get_device_properties(q.device).multi_processor_count
@@ -113,7 +120,7 @@ def test_persistent_nc_tail_split(kind):
     fa = _fa()
     b, h, s = 1, 48, 2048
     q, k, v = (_rand((b, h, s, 128), 300 + i) for i in range(3))
-    out_base = fa.flash_attention_fwd(q, k, v, causal=False, config=8)
+    out_base = fa.flash_attention_fwd(q, k, v, causal=False, config=_base_ids()[False])
     out = fa.flash_attention_fwd(q, k, v, causal=False, config=_ids(kind)[False])
     torch.cuda.synchronize()
     assert (out.float() - out_base.float()).abs().max().item() <= TOL
