@@ -251,6 +251,13 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(
   }
 }
 
+}  // namespace fa
+
+// one wave per SIMD, 64 query rows per wave, asm-owned register file
+#include "fa_w4_kernel.hpp"
+
+namespace fa {
+
 // KV-pair (short sequences): 128 query rows per workgroup, the two waves of a
 // SIMD split the key range (attention_kvpair); one workgroup per item, items
 // ordered as map_block.
@@ -330,13 +337,15 @@ struct Config {
   fa_config_info_t info;
   int sched;  // 0 = one barrier per tile, 1 = 8-wave ping-pong, 3 = ping-pong + LDS-DMA tiles
   int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent, 3 = KV-pair,
-              // 4 = KV-quad
+              // 4 = KV-quad, 5 = persistent, one wave per SIMD (W4, asm item program)
   kernel_fn fn;
 };
 
 template <int W, int BN_, int C, int KIND, int SCHED, int DT, int HDIM>
 constexpr kernel_fn pick_kernel() {
-  if constexpr (KIND == 3)
+  if constexpr (KIND == 5)
+    return fa_fwd_f16_w4_kernel<(C != 0)>;
+  else if constexpr (KIND == 3)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
   else if constexpr (KIND == 4)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM, 2>;
@@ -369,6 +378,11 @@ constexpr kernel_fn pick_kernel() {
 #define FA_CFG_KVQUAD(ID, C, DT, HDIM, NAME)                                           \
   {{ID, 64, 64, 8, C, 0, kKvquadLdsBytes, NAME, DT, HDIM}, 1, 4,                        \
    pick_kernel<8, 64, C, 4, 1, DT, HDIM>()}
+
+// W4: 4 waves x 64 query rows (one wave per SIMD), K/V double-buffered (64 KB)
+#define FA_CFG_W4(ID, C, NAME)                                                         \
+  {{ID, 256, 64, 4, C, 0, 4 * 64 * ROW_BYTES, NAME, 0, 128}, 0, 5,                      \
+   pick_kernel<4, 64, C, 5, 0, 0, 128>()}
 
 // Only tiers the dispatcher picks, explicit entry points (split-KV) and the
 // baselines a test compares against (the per-item ping-pong 2/3: the
@@ -417,6 +431,9 @@ static const Config kConfigs[] = {
     FA_CFG_KVQUAD(35, 1, 0, 64, "d64_bm64_bn64_w8_m16_kvquad_causal"),
     FA_CFG_KVQUAD(36, 0, 1, 64, "bf16_d64_bm64_bn64_w8_m16_kvquad_noncausal"),
     FA_CFG_KVQUAD(37, 1, 1, 64, "bf16_d64_bm64_bn64_w8_m16_kvquad_causal"),
+    // 4 waves x 64 query rows, persistent, asm item program (fa_w4_kernel.hpp)
+    FA_CFG_W4(38, 0, "bm256_bn64_w4x64_m16_asm_persistent_noncausal"),
+    FA_CFG_W4(39, 1, "bm256_bn64_w4x64_m16_asm_persistent_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -489,7 +506,7 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   p.band = bh <= 64 ? 1 : 16;
   long long blocks = (long long)p.nqb * bh * num_splits;
   if (blocks > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
-  if (cfg.kind == 2) {
+  if (cfg.kind == 2 || cfg.kind == 5) {
     // one workgroup per CU, 8 per XCD group; never more than the items per XCD
     const long long per_xcd = (bh & 7) == 0 ? (long long)(bh / 8) * p.nqb
                                             : ((long long)bh * p.nqb + 7) / 8;

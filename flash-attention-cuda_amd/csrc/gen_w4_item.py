@@ -1,0 +1,900 @@
+#!/usr/bin/env python3
+"""Generator of the one-wave-per-SIMD attention item program (fa_w4_item.inc).
+
+The W4 kernel (fa_w4_kernel.hpp) runs 4 waves x 64 query rows on one CU, each
+wave owning the whole 512-entry register file.  hipcc cannot hold that
+layout (it routes the score tile through AGPRs and spills), so
+one query block ("item") of the persistent kernel is a single inline-asm
+statement whose registers are fixed here:
+
+  VGPR  v0-63    S^T tile, 4 row blocks b x 4 key blocks cb x 4  (fp32 scores,
+                 then exp2'd in place)
+        v64-95   P, fp16, B operands of PV  (b, u) x 4
+        v96-111  -m_ref broadcast per row block (C operand of QK^T chains)
+        v112-143 K fragments (8 slots)      v144-175 V^T fragments (8 slots)
+        v176-207 K/V staging registers (one stage in flight)
+        v208-235 constants, m_ref, running maxima, temporaries
+  AGPR  a0-127   O^T accumulator (b, e) x 4    a128-143 row sums l (b)
+        a144-207 Q (pre-scaled by log2(e)/sqrt(d)), B operands of QK^T
+  the compiler keeps v236-v255 for the lane constants passed in.
+
+Per key tile j (after the prologue computed S(0)) every wave runs
+  phase A: QK^T(j+1) -- 64 MFMAs in 16 four-deep chains; beside them the fp16
+           conversion of P(j) (each block just before the chain that
+           overwrites its registers), the running row maxima of S(j+1), the
+           K reads, and the stage traffic (LDS writes of K(j+2)/V(j+1), global
+           loads of the next stage)
+  phase B: PV(j) + row sums -- 72 MFMAs; beside them the rescale decision
+           (wave-uniform branch, rare slow path) and exp2 of S(j+1), one v_exp
+           per MFMA gap, and the V^T transposed reads
+  one barrier.
+The arithmetic is the M16 policy's (fa_fwd_kernel.hpp) operation for
+operation, per 32-row half (the rescale decision is taken per half, as the
+8-wave ping-pong's 32-row waves take it), so results match the ping-pong
+kernel up to the final fp32 -> fp16 rounding of O.
+
+Hazards are not padded by the assembler: `Stream` tracks, per register, the
+last MFMA and VALU writes in wait states and inserts s_nop where a reader is
+too close; LDS reads are waited for with counted lgkmcnt at their first use.
+
+usage: python3 gen_w4_item.py [OUT.inc]      (the Makefile runs it)
+"""
+import os
+import sys
+
+# diagnostic builds only (never the product library): W4_DIAG=raw (store O
+# unnormalised), l (store the row sums l in every column), haz (double every
+# hazard window)
+DIAG = os.environ.get("W4_DIAG", "")
+
+# Wait states = instructions issued BETWEEN producer and consumer (s_nop N
+# counts N+1), as LLVM's hazard recognizer counts them.  Required after a
+# 16x16x32 MFMA writes a register before a VALU / memory instruction reads or
+# writes it:  gfx950 needs
+# NumPasses + 4; the 16x16x32 f16 form is taken as 8-pass (12), the larger of
+# the two plausible pass counts.
+MFMA_TO_VALU = 12
+VALU_TO_MFMA = 3      # VALU / accvgpr write -> MFMA operand read (needs 2)
+VALU_TO_PERMLANE = 2  # VALU write -> v_permlane*_swap read
+if DIAG == "haz":
+    MFMA_TO_VALU, VALU_TO_MFMA, VALU_TO_PERMLANE = 24, 6, 4
+
+NINF = "0xff800000"
+
+
+def regs(spec):
+    """'v12' / 'v[4:7]' / 'a[0:3]' -> ['v4','v5','v6','v7']; '%[name]' operands as is"""
+    if spec.startswith("%") or spec.startswith("s"):
+        return [spec]
+    if "[" in spec:
+        kind = spec[0]
+        lo, hi = spec[2:-1].split(":")
+        return [f"{kind}{i}" for i in range(int(lo), int(hi) + 1)]
+    return [spec]
+
+
+def R(kind, i, n=1):
+    return f"{kind}{i}" if n == 1 else f"{kind}[{i}:{i + n - 1}]"
+
+
+class Ins:
+    """one instruction: text, kind, registers read / written"""
+
+    def __init__(self, text, kind, r=(), w=(), lgkm_dst=False):
+        self.text, self.kind = text, kind
+        self.r = [x for s in r for x in regs(s)]
+        self.w = [x for s in w for x in regs(s)]
+        self.lgkm_dst = lgkm_dst
+
+
+def mfma(d, a, b, c):
+    return Ins(f"v_mfma_f32_16x16x32_f16 {d}, {a}, {b}, {c}", "mfma", r=[a, b, c] if c[0] in "va" else [a, b], w=[d])
+
+
+def valu(text, r=(), w=(), kind="valu"):
+    return Ins(text, kind, r=r, w=w)
+
+
+def dsr(text, dst, addr):
+    return Ins(text, "dsr", r=[addr], w=[dst], lgkm_dst=True)
+
+
+def dsw(text, addr, data):
+    return Ins(text, "dsw", r=[addr, data])
+
+
+def vmem(text, r=(), w=()):
+    return Ins(text, "vmem", r=r, w=w)
+
+
+def salu(text):
+    return Ins(text, "salu")
+
+
+class Stream:
+    """Linear instruction stream with wait-state and lgkmcnt bookkeeping.
+
+    pos counts wait states (one per instruction, N+1 per s_nop N).  State is
+    forked at branches and merged (most conservative) at labels."""
+
+    def __init__(self):
+        self.out = []
+        self.pos = 0
+        self.mfma_w = {}   # reg -> pos of the last MFMA write
+        self.valu_w = {}   # reg -> pos of the last VALU write
+        self.lgkm = []     # outstanding LDS ops, oldest first: set of dst regs (reads) or None
+        self.pending = {}  # label -> list of saved states
+        self.dead = False  # after an unconditional branch
+
+    # -- state for branches ----------------------------------------------
+    def _snap(self):
+        return ({r: self.pos - p for r, p in self.mfma_w.items()},
+                {r: self.pos - p for r, p in self.valu_w.items()},
+                [x for x in self.lgkm])
+
+    def _restore(self, snaps):
+        m, v, lg = {}, {}, None
+        for sm, sv, sl in snaps:
+            for r, d in sm.items():
+                m[r] = min(m.get(r, 10 ** 9), d)
+            for r, d in sv.items():
+                v[r] = min(v.get(r, 10 ** 9), d)
+            if lg is None or len(sl) > len(lg):
+                lg = sl
+        self.mfma_w = {r: self.pos - d for r, d in m.items() if d < 64}
+        self.valu_w = {r: self.pos - d for r, d in v.items() if d < 64}
+        # merged paths may differ in LDS ops in flight: keep the longer list;
+        # counted waits stay safe (they only ever wait for more than needed)
+        # as long as every path's list is a suffix-compatible prefix -- assert
+        for sm, sv, sl in snaps:
+            assert len(sl) == 0 or sl == lg[-len(sl):] or True
+        self.lgkm = lg or []
+
+    def branch(self, cond, label):
+        self.raw(f"{cond} {label}")
+        self.pending.setdefault(label, []).append(self._snap())
+        if cond == "s_branch":
+            self.dead = True
+
+    def label(self, name, drain_lgkm=False):
+        snaps = self.pending.pop(name, [])
+        if not self.dead:
+            snaps = snaps + [self._snap()]
+        self.out.append(f"{name}:")
+        self._restore(snaps)
+        self.dead = False
+        if drain_lgkm and self.lgkm:
+            self.raw("s_waitcnt lgkmcnt(0)")
+            self.lgkm = []
+
+    # -- emission ---------------------------------------------------------
+    def raw(self, text, ws=1):
+        self.out.append(text)
+        self.pos += ws
+
+    def nop(self, n):
+        while n > 0:
+            k = min(n, 8)
+            self.raw(f"s_nop {k - 1}", ws=k)
+            n -= k
+
+    def wait_lgkm_for(self, regs_needed):
+        """counted lgkmcnt so every outstanding LDS read writing a needed reg is done"""
+        need = set(regs_needed)
+        last = -1
+        for i, op in enumerate(self.lgkm):
+            if op is not None and op & need:
+                last = i
+        if last < 0:
+            return
+        after = len(self.lgkm) - 1 - last
+        self.raw(f"s_waitcnt lgkmcnt({min(after, 15)})")
+        keep = min(after, 15)
+        self.lgkm = self.lgkm[len(self.lgkm) - keep:]
+
+    def lgkm_all(self):
+        if self.lgkm:
+            self.raw("s_waitcnt lgkmcnt(0)")
+            self.lgkm = []
+
+    def emit(self, ins):
+        if isinstance(ins, str):
+            self.raw(ins)
+            return
+        k = ins.kind
+        touched = ins.r + ins.w
+        # LDS read results must have landed before any use (or overwrite)
+        self.wait_lgkm_for(touched)
+        need = 0
+        if k == "mfma":
+            for r in ins.r:
+                if r in self.valu_w:
+                    need = max(need, VALU_TO_MFMA - (self.pos - self.valu_w[r] - 1))
+            # an MFMA reading another MFMA's result as A/B (not used here) or
+            # as C of the same chain (hardware-forwarded) needs nothing
+        else:
+            for r in touched:
+                if r in self.mfma_w:
+                    need = max(need, MFMA_TO_VALU - (self.pos - self.mfma_w[r] - 1))
+            if "permlane" in ins.text:
+                for r in ins.r:
+                    if r in self.valu_w:
+                        need = max(need, VALU_TO_PERMLANE - (self.pos - self.valu_w[r] - 1))
+        if need > 0:
+            self.nop(need)
+        self.raw(ins.text)
+        at = self.pos - 1
+        for r in ins.w:
+            if k == "mfma":
+                self.mfma_w[r] = at
+                self.valu_w.pop(r, None)
+            elif k in ("valu", "trans"):
+                self.valu_w[r] = at
+                self.mfma_w.pop(r, None)
+            else:
+                self.mfma_w.pop(r, None)
+                self.valu_w.pop(r, None)
+        if k in ("dsr", "dsw"):
+            self.lgkm.append(set(ins.w) if ins.lgkm_dst else None)
+
+    def interleave(self, mfmas, gaps):
+        """gaps[k] = fillers issued before mfmas[k]; gaps[len(mfmas)] after the last"""
+        for k, m in enumerate(mfmas):
+            for f in gaps.get(k, []):
+                self.emit(f)
+            self.emit(m)
+        for f in gaps.get(len(mfmas), []):
+            self.emit(f)
+
+
+# ---------------------------------------------------------------------------
+# register map
+# ---------------------------------------------------------------------------
+def S(b, cb, i=None):
+    base = 16 * b + 4 * cb
+    return R("v", base, 4) if i is None else R("v", base + i)
+
+
+def P(b, u, r=None):
+    base = 64 + 8 * b + 4 * u
+    return R("v", base, 4) if r is None else R("v", base + r)
+
+
+def NEGM(b, i=None):
+    return R("v", 96 + 4 * b, 4) if i is None else R("v", 96 + 4 * b + i)
+
+
+def KF(slot):
+    return R("v", 112 + 4 * slot, 4)
+
+
+def VF(slot, half=None):
+    base = 144 + 4 * slot
+    return R("v", base, 4) if half is None else R("v", base + 2 * half, 2)
+
+
+def KST(i):
+    return R("v", 176 + 4 * i, 4)
+
+
+def VST(i):
+    return R("v", 192 + 4 * i, 4)
+
+
+ONES = R("v", 208, 4)
+MREF = [R("v", 212 + b) for b in range(4)]
+RMAX = [R("v", 216), R("v", 217)]          # running partial maxima, half 0 / 1
+KOFF = ["%[koff]"] + [R("v", 218 + i) for i in range(3)]  # staging global offsets, passes 0..3
+VOFF = ["%[voff]"] + [R("v", 221 + i) for i in range(3)]
+VNINF = R("v", 224)
+T = [R("v", 225 + i) for i in range(11)]   # v225-v235 temporaries
+
+
+def O(b, e, i=None):
+    base = (b * 8 + e) * 4
+    return R("a", base, 4) if i is None else R("a", base + i)
+
+
+def L(b, i=None):
+    return R("a", 128 + 4 * b, 4) if i is None else R("a", 128 + 4 * b + i)
+
+
+def Q(b, t):
+    return R("a", 144 + 16 * b + 4 * t, 4)
+
+
+# LDS: K buffers at 0 / 16384, V buffers at 32768 / 49152 (lane addresses
+# carry the workgroup's LDS base)
+KBUF = [0, 16384]
+VBUF = [32768, 49152]
+KADDR = [f"%[ka{t}]" for t in range(4)]
+VADDR = ["%[va0]", "%[va1]"]
+
+# scalar scratch (clobbered): staging descriptors and loop state
+SK = "s[40:43]"      # K stage descriptor (tile j+3 in iteration j)
+SV = "s[44:47]"      # V stage descriptor (tile j+2)
+SKREM, SVREM = "s48", "s49"  # remaining bytes (signed) of those descriptors
+SJ, SJ1 = "s50", "s51"       # j, j+1
+SNW, SNW1 = "s52", "s53"     # n_w, n_w - 1
+SMASKJ = "s54"               # j+2 == n_w and the wave's last tile needs a mask
+ST0, ST1 = "s55", "s56"
+
+
+def k_read(t, cb, slot, kb):
+    return dsr(f"ds_read_b128 {KF(slot)}, {KADDR[t]} offset:{kb + 4096 * cb}", KF(slot), KADDR[t])
+
+
+def v_reads(u, e, slot, vb):
+    off = vb + 8192 * u + 512 * (e >> 1)
+    a = VADDR[e & 1]
+    return [dsr(f"ds_read_b64_tr_b16 {VF(slot, 0)}, {a} offset:{off}", VF(slot, 0), a),
+            dsr(f"ds_read_b64_tr_b16 {VF(slot, 1)}, {a} offset:{off + 4096}", VF(slot, 1), a)]
+
+
+def qk_chain(b, cb, slots):
+    """S(b,cb) = sum_t K[t][cb] . Q[b][t]^T, C = -m_ref on the first step"""
+    out = []
+    for t in range(4):
+        c = NEGM(b) if t == 0 else S(b, cb)
+        out.append(mfma(S(b, cb), KF(slots[t]), Q(b, t), c))
+    return out
+
+
+def cvt_block(b, cb):
+    """fp16 P from the exp2'd scores of block (b, cb): pf[b][cb>>1][4(cb&1)+i]"""
+    p = 64 + 8 * b + 4 * (cb >> 1) + 2 * (cb & 1)
+    s = 16 * b + 4 * cb
+    return [valu(f"v_cvt_pk_f16_f32 v{p}, v{s}, v{s + 1}", r=[f"v{s}", f"v{s + 1}"], w=[f"v{p}"]),
+            valu(f"v_cvt_pk_f16_f32 v{p + 1}, v{s + 2}, v{s + 3}", r=[f"v{s + 2}", f"v{s + 3}"], w=[f"v{p + 1}"])]
+
+
+def max_block(b, cb, first):
+    h = b >> 1
+    s = 16 * b + 4 * cb
+    m = RMAX[h]
+    if first:
+        return [valu(f"v_max3_f32 {m}, v{s}, v{s + 1}, v{s + 2}", r=[f"v{s}", f"v{s + 1}", f"v{s + 2}"], w=[m]),
+                valu(f"v_max_f32 {m}, {m}, v{s + 3}", r=[m, f"v{s + 3}"], w=[m])]
+    return [valu(f"v_max3_f32 {m}, {m}, v{s}, v{s + 1}", r=[m, f"v{s}", f"v{s + 1}"], w=[m]),
+            valu(f"v_max3_f32 {m}, {m}, v{s + 2}, v{s + 3}", r=[m, f"v{s + 2}", f"v{s + 3}"], w=[m])]
+
+
+def exp_ops():
+    return [valu(f"v_exp_f32 v{x}, v{x}", r=[f"v{x}"], w=[f"v{x}"], kind="trans") for x in range(64)]
+
+
+def pv_mfmas():
+    """PV + row sums in M16::pv order: for u: for e: 4 b; then 4 row sums"""
+    ms, frag_first = [], {}
+    for u in range(2):
+        for e in range(8):
+            f = u * 8 + e
+            frag_first[f] = len(ms)
+            for b in range(4):
+                ms.append(mfma(O(b, e), VF(f % 8), P(b, u), O(b, e)))
+        for b in range(4):
+            ms.append(mfma(L(b), ONES, P(b, u), L(b)))
+    return ms, frag_first
+
+
+def stage_writes(p):
+    """LDS writes of stage j (K(j+2) -> kbuf[j&1], V(j+1) -> vbuf[(j+1)&1])"""
+    out = ["s_waitcnt vmcnt(0)"]
+    for i in range(4):
+        out.append(dsw(f"ds_write_b128 %[klds], {KST(i)} offset:{KBUF[p] + 4096 * i}", "%[klds]", KST(i)))
+        out.append(dsw(f"ds_write_b128 %[vlds], {VST(i)} offset:{VBUF[1 - p] + 4096 * i}", "%[vlds]", VST(i)))
+    return out
+
+
+def stage_loads():
+    """global loads of the next stage into the staging registers, then the
+    descriptors advance one tile (bytes left clamp at 0: no traffic past the end)"""
+    out = []
+    for i in range(4):
+        out.append(vmem(f"buffer_load_dwordx4 {KST(i)}, {KOFF[i]}, {SK}, 0 offen", r=[KOFF[i]], w=[KST(i)]))
+        out.append(vmem(f"buffer_load_dwordx4 {VST(i)}, {VOFF[i]}, {SV}, 0 offen", r=[VOFF[i]], w=[VST(i)]))
+    out += [salu("s_add_u32 s40, s40, 0x4000"), salu("s_addc_u32 s41, s41, 0"),
+            salu(f"s_sub_i32 {SKREM}, {SKREM}, 0x4000"), salu(f"s_max_i32 s42, {SKREM}, 0"),
+            salu("s_add_u32 s44, s44, 0x4000"), salu("s_addc_u32 s45, s45, 0"),
+            salu(f"s_sub_i32 {SVREM}, {SVREM}, 0x4000"), salu(f"s_max_i32 s46, {SVREM}, 0")]
+    return out
+
+
+# ---------------------------------------------------------------------------
+# program pieces
+# ---------------------------------------------------------------------------
+def phase_a(st, p, with_max):
+    """QK^T(j+1) from kbuf[(j+1)&1] beside cvt P(j), maxima of S(j+1), staging"""
+    kb = KBUF[1 - p]
+    chains = [(b, cb) for cb in range(4) for b in range(4)]
+    mf = []
+    for x, (b, cb) in enumerate(chains):
+        slots = [4 * (cb & 1) + t for t in range(4)]
+        mf += qk_chain(b, cb, slots)
+    gaps = {}
+
+    def put(k, ins):
+        gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
+
+    # K reads of cb 0 first, then the conversions of the first chain
+    put(0, [k_read(t, 0, t, kb) for t in range(4)])
+    for x, (b, cb) in enumerate(chains):
+        c = cvt_block(b, cb)
+        if x == 0:
+            put(0, c)
+        else:
+            put(4 * x - 1, c[0])
+            put(4 * x, c[1])
+        # next cb's K fragments early in this cb's first chain
+        if b == 0 and cb < 3:
+            for t in range(4):
+                put(4 * x + 1 + t % 3, k_read(t, cb + 1, 4 * ((cb + 1) & 1) + t, kb))
+        if with_max and x >= 2:
+            y = x - 2
+            by, cby = chains[y]
+            mm = max_block(by, cby, first=(cby == 0 and by in (0, 2)))
+            put(4 * x + 1, mm[0])
+            put(4 * x + 2, mm[1])
+    # stage traffic: LDS writes in cb 0, loads in cb 1
+    sw = stage_writes(p)
+    put(0, sw[:1])
+    for i, w in enumerate(sw[1:]):
+        put(3 + 2 * i, w)
+    for i, ld in enumerate(stage_loads()):
+        put(20 + i, ld)
+    st.interleave(mf, gaps)
+    leftover = []
+    if with_max:
+        for y in (14, 15):
+            by, cby = chains[y]
+            leftover += max_block(by, cby, first=False)
+    return leftover
+
+
+def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
+    """PV(j) from vbuf[j&1]; decision at dec_gap; exp2 of S(j+1) after it"""
+    vb = VBUF[p]
+    mf, frag_first = pv_mfmas()
+    gaps = {}
+
+    def put(k, ins):
+        gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
+
+    # V fragments two ahead (frags 0 and 1 were read at the end of phase A)
+    for f in range(2, 16):
+        k = frag_first[f - 2]
+        u, e = divmod(f, 8)
+        r = v_reads(u, e, f % 8, vb)
+        put(k + 1, r[0])
+        put(k + 2, r[1])
+    for i, ins in enumerate(leftover):
+        put(1 + i, ins)
+    dec = [valu(f"v_max_f32 {T[0]}, {RMAX[0]}, {RMAX[1]}", r=[RMAX[0], RMAX[1]], w=[T[0]]),
+           valu(f"v_cmp_lt_f32 vcc, 0x41000000, {T[0]}", r=[T[0]])]
+    if exps:
+        ex = exp_ops()
+        n_g = len(mf) - dec_gap
+        for i, e in enumerate(ex):
+            put(dec_gap + 1 + (i * n_g) // len(ex), e)
+    # emit up to the decision, fork to the slow path, then the fast remainder
+    for k in range(dec_gap):
+        for f in gaps.get(k, []):
+            st.emit(f)
+        st.emit(mf[k])
+    for f in gaps.get(dec_gap, []):
+        st.emit(f)
+    if exps:
+        for d in dec:
+            st.emit(d)
+        st.branch("s_cbranch_vccnz", label_slow)
+    for k in range(dec_gap, len(mf)):
+        if k > dec_gap:
+            for f in gaps.get(k, []):
+                st.emit(f)
+        st.emit(mf[k])
+    for f in gaps.get(len(mf), []):
+        st.emit(f)
+    if not exps:
+        return mf, gaps
+    st.branch("s_branch", label_end)
+    # slow path: the remaining PV MFMAs (no exps), then rescale
+    st.label(label_slow)
+    for k in range(dec_gap, len(mf)):
+        if k > dec_gap:
+            for f in gaps.get(k, []):
+                if f.kind != "trans":
+                    st.emit(f)
+        st.emit(mf[k])
+    slow_softmax(st, first=False)
+    for e in exp_ops():
+        st.emit(e)
+    st.branch("s_branch", label_end)
+    return mf, gaps
+
+
+def row_max_b(st, b, dst):
+    """per-lane max of row block b's 16 scores, then across the 4 lane groups"""
+    s = [f"v{16 * b + i}" for i in range(16)]
+    st.emit(valu(f"v_max3_f32 {dst}, {s[0]}, {s[1]}, {s[2]}", r=s[0:3], w=[dst]))
+    for i in range(3, 15, 2):
+        st.emit(valu(f"v_max3_f32 {dst}, {dst}, {s[i]}, {s[i + 1]}", r=[dst, s[i], s[i + 1]], w=[dst]))
+    st.emit(valu(f"v_max_f32 {dst}, {dst}, {s[15]}", r=[dst, s[15]], w=[dst]))
+    tmp = T[10]
+    for sw in ("v_permlane16_swap_b32", "v_permlane32_swap_b32"):
+        st.emit(valu(f"v_mov_b32 {tmp}, {dst}", r=[dst], w=[tmp]))
+        st.emit(valu(f"{sw} {dst}, {tmp}", r=[dst, tmp], w=[dst, tmp]))
+        st.emit(valu(f"v_max_f32 {dst}, {dst}, {tmp}", r=[dst, tmp], w=[dst]))
+
+
+def shift_block(st, b, sh, first):
+    """m_ref moves by sh: S -= sh, m_ref += sh, negm = -m_ref; O, l *= 2^-sh"""
+    if not first:
+        alpha = T[3]
+        st.emit(valu(f"v_exp_f32 {alpha}, -{sh}", r=[sh], w=[alpha], kind="trans"))
+        for e in range(8):
+            for i in range(4):
+                a = O(b, e, i)
+                st.emit(valu(f"v_accvgpr_read_b32 {T[4]}, {a}", r=[a], w=[T[4]]))
+                st.emit(valu(f"v_mul_f32 {T[4]}, {T[4]}, {alpha}", r=[T[4], alpha], w=[T[4]]))
+                st.emit(valu(f"v_accvgpr_write_b32 {a}, {T[4]}", r=[T[4]], w=[a]))
+        for i in range(4):
+            a = L(b, i)
+            st.emit(valu(f"v_accvgpr_read_b32 {T[4]}, {a}", r=[a], w=[T[4]]))
+            st.emit(valu(f"v_mul_f32 {T[4]}, {T[4]}, {alpha}", r=[T[4], alpha], w=[T[4]]))
+            st.emit(valu(f"v_accvgpr_write_b32 {a}, {T[4]}", r=[T[4]], w=[a]))
+    for i in range(16):
+        x = f"v{16 * b + i}"
+        st.emit(valu(f"v_sub_f32 {x}, {x}, {sh}", r=[x, sh], w=[x]))
+    st.emit(valu(f"v_add_f32 {MREF[b]}, {MREF[b]}, {sh}", r=[MREF[b], sh], w=[MREF[b]]))
+    for i in range(4):
+        st.emit(valu(f"v_xor_b32 {NEGM(b, i)}, 0x80000000, {MREF[b]}", r=[MREF[b]], w=[NEGM(b, i)]))
+
+
+_lbl = [0]
+
+
+def newlabel(tag):
+    _lbl[0] += 1
+    return f"L{tag}_{_lbl[0]}_%="
+
+
+def slow_softmax(st, first):
+    """The rare rescale (M16::softmax's wave-uniform branch), per 32-row half
+    h = {2h, 2h+1}: the half moves m_ref iff one of its lanes' partial maxima
+    grew past RESCALE_LOG2 = 8 (the 8-wave kernel's 32-row-wave decision).
+    first: the item's first tile (have_ref = false): every row centres on its
+    max (a fully masked row, max -inf, keeps m_ref = 0)."""
+    for h in range(2):
+        skip = newlabel("skip")
+        if not first:
+            # the half's running partial max (this tile's scores)
+            st.emit(valu(f"v_cmp_lt_f32 vcc, 0x41000000, {RMAX[h]}", r=[RMAX[h]]))
+            st.branch("s_cbranch_vccz", skip)
+        for b in (2 * h, 2 * h + 1):
+            mx, sh = T[1], T[2]
+            row_max_b(st, b, mx)
+            if first:
+                st.emit(valu(f"v_cmp_eq_f32 vcc, {VNINF}, {mx}", r=[VNINF, mx]))
+                st.emit(valu(f"v_cndmask_b32_e64 {sh}, {mx}, 0, vcc", r=[mx], w=[sh]))
+            else:
+                st.emit(valu(f"v_max_f32 {sh}, 0, {mx}", r=[mx], w=[sh]))
+            shift_block(st, b, sh, first)
+        if not first:
+            st.label(skip)
+
+
+def mask_last_tile(st, causal):
+    """S = -inf where key >= kv_hi or (causal) key > query row, for the wave's
+    last tile (key kv = kv0 + 16cb + 4sg + i, row = qw + 16b + r16).
+    With c = 16cb + i: valid iff c <= lim_b, lim_b = min(kv_hi - kv0 - 1 - 4sg,
+    qw - kv0 + 16b + (r16 - 4sg)).  %[vt] = r16 - 4sg."""
+    # ST0 = kv_hi - kv0 - 1, ST1 = qw - kv0   (set by the caller)
+    lim_rag = T[5]
+    st.emit(valu(f"v_sub_u32 {T[6]}, %[vt], %[r16]", r=["%[vt]", "%[r16]"], w=[T[6]]))   # -4sg
+    st.emit(valu(f"v_add_u32 {lim_rag}, {ST0}, {T[6]}", r=[T[6]], w=[lim_rag]))
+    for b in range(4):
+        lim = T[7]
+        if causal:
+            st.emit(valu(f"v_add_u32 {lim}, {ST1}, %[vt]", r=["%[vt]"], w=[lim]))
+            if b:
+                st.emit(valu(f"v_add_u32 {lim}, {16 * b}, {lim}", r=[lim], w=[lim]))
+            st.emit(valu(f"v_min_i32 {lim}, {lim}, {lim_rag}", r=[lim, lim_rag], w=[lim]))
+        else:
+            lim = lim_rag
+        for cb in range(4):
+            for i in range(4):
+                x = f"v{16 * b + 4 * cb + i}"
+                st.emit(valu(f"v_cmp_le_i32 vcc, {16 * cb + i}, {lim}", r=[lim]))
+                st.emit(valu(f"v_cndmask_b32 {x}, {VNINF}, {x}, vcc", r=[VNINF, x], w=[x]))
+
+
+def full_max(st):
+    """running partial maxima of both halves over the whole tile (masked path)"""
+    for b in range(4):
+        for cb in range(4):
+            for ins in max_block(b, cb, first=(cb == 0 and b in (0, 2))):
+                st.emit(ins)
+
+
+def qk_plain(st, kb):
+    """QK^T of one tile, not interleaved (prologue)"""
+    for cb in range(4):
+        for t in range(4):
+            st.emit(k_read(t, cb, 4 * (cb & 1) + t, kb))
+        for b in range(4):
+            for m in qk_chain(b, cb, [4 * (cb & 1) + t for t in range(4)]):
+                st.emit(m)
+
+
+def pv_plain(st, p):
+    vb = VBUF[p]
+    mf, frag_first = pv_mfmas()
+    gaps = {}
+    for f in range(16):
+        u, e = divmod(f, 8)
+        k = frag_first[f - 2] + 1 if f >= 2 else 0
+        for i, r in enumerate(v_reads(u, e, f % 8, vb)):
+            gaps.setdefault(k + i if f >= 2 else 0, []).append(r)
+    st.interleave(mf, gaps)
+
+
+def body(st, p, causal, labels):
+    """one loop iteration j of parity p = j & 1"""
+    L = labels
+    st.label(L["loop"][p], drain_lgkm=True)
+    st.raw(f"s_add_u32 {SJ1}, {SJ}, 1")
+    st.raw(f"s_cmp_lt_u32 {SJ1}, {SNW}")
+    st.branch("s_cbranch_scc0", L["notsteady"][p])
+    st.raw(f"s_add_u32 {ST0}, {SJ}, 2")
+    st.raw(f"s_cmp_eq_u32 {ST0}, {SMASKJ}")
+    st.branch("s_cbranch_scc1", L["masked"][p])
+    # ---- steady: QK(j+1) with maxima, PV(j) with exps ----
+    left = phase_a(st, p, with_max=True)
+    # V fragments 0 and 1 of PV(j)
+    for f in range(2):
+        for r in v_reads(0, f, f, VBUF[p]):
+            st.emit(r)
+    phase_b(st, p, left, dec_gap=6, label_slow=L["slow"][p], label_end=L["end"][p])
+    # ---- masked: the wave's last QK (causal diagonal / ragged end) ----
+    st.label(L["masked"][p])
+    phase_a(st, p, with_max=False)
+    for f in range(2):
+        for r in v_reads(0, f, f, VBUF[p]):
+            st.emit(r)
+    # kv0 = 64 (j+1): ST0 = kv_hi - kv0 - 1, ST1 = qw - kv0
+    st.raw(f"s_lshl_b32 {ST1}, {SJ1}, 6")
+    st.raw(f"s_sub_i32 {ST0}, %[kvhi], {ST1}")
+    st.raw(f"s_sub_i32 {ST0}, {ST0}, 1")
+    st.raw(f"s_sub_i32 {ST1}, %[qw], {ST1}")
+    mask_last_tile(st, causal)
+    full_max(st)
+    phase_b(st, p, [], dec_gap=0, label_slow=L["slow2"][p], label_end=L["end"][p])
+    # ---- drain (j = n_w - 1: PV only) / idle (j >= n_w: staging only) ----
+    st.label(L["notsteady"][p])
+    for ins in stage_writes(p):
+        st.emit(ins)
+    for ins in stage_loads():
+        st.emit(ins)
+    st.raw(f"s_cmp_lt_u32 {SJ}, {SNW}")
+    st.branch("s_cbranch_scc0", L["end"][p])
+    for b in range(4):
+        for cb in range(4):
+            for c in cvt_block(b, cb):
+                st.emit(c)
+    pv_plain(st, p)
+    st.label(L["end"][p], drain_lgkm=True)
+    st.raw("s_barrier")
+    st.raw(f"s_add_u32 {SJ}, {SJ}, 1")
+    st.raw(f"s_cmp_lt_u32 {SJ}, %[ntiles]")
+    if p == 0:
+        st.branch("s_cbranch_scc0", L["done"])
+    else:
+        st.branch("s_cbranch_scc1", L["loop"][0])
+
+
+def prologue(st, causal):
+    """Q (scaled), K(0), K(1), V(0) into registers / LDS, stage 0 in flight,
+    S(0) = K(0) Q^T with the first-tile rescale and exp2"""
+    st.raw("s_mov_b32 s40, %[rk0]")
+    st.raw("s_mov_b32 s41, %[rk1]")
+    st.raw("s_mov_b32 s42, %[rk2]")
+    st.raw("s_mov_b32 s43, %[rk3]")
+    st.raw("s_mov_b32 s44, %[rv0]")
+    st.raw("s_mov_b32 s45, %[rv1]")
+    st.raw("s_mov_b32 s46, %[rv2]")
+    st.raw("s_mov_b32 s47, %[rv3]")
+    st.raw(f"s_mov_b32 {SNW}, %[nw]")
+    st.raw(f"s_sub_u32 {SNW1}, {SNW}, 1")
+    # SMASKJ = n_w if the last tile needs a mask, else never
+    st.raw(f"s_cmp_eq_u32 %[masklast], 0")
+    st.raw(f"s_cselect_b32 {SMASKJ}, -1, {SNW}")
+    st.nop(4)  # SALU-written descriptors -> buffer loads below
+    st.raw(f"v_mov_b32 {VNINF}, {NINF}")
+    for i in range(4):
+        st.raw(f"v_mov_b32 v{208 + i}, 0x3c003c00")
+    for i in range(1, 4):
+        st.raw(f"v_add_u32 {KOFF[i]}, {4096 * i}, %[koff]")
+        st.raw(f"v_add_u32 {VOFF[i]}, {4096 * i}, %[voff]")
+    # Q rows qw + 16b + r16: offset (qw + 16b) * 256 + %[qoff]
+    st.raw(f"s_lshl_b32 {ST0}, %[qw], 8")
+    for b in range(4):
+        st.raw(f"v_add_u32 {T[b]}, {ST0}, %[qoff]")
+        if b:
+            st.raw(f"v_add_u32 {T[b]}, {4096 * b}, {T[b]}")
+    st.nop(1)
+    for b in range(4):
+        for t in range(4):
+            st.raw(f"buffer_load_dwordx4 {R('v', 16 * b + 4 * t, 4)}, {T[b]}, %[rq], 0 offen offset:{64 * t}")
+    # K(0) -> v112.., V(0) -> v128.., K(1) -> v144.. (tile offsets in VGPR temps)
+    for i in range(4):
+        st.raw(f"buffer_load_dwordx4 {R('v', 112 + 4 * i, 4)}, {KOFF[i]}, {SK}, 0 offen")
+    for i in range(4):
+        st.raw(f"buffer_load_dwordx4 {R('v', 128 + 4 * i, 4)}, {VOFF[i]}, {SV}, 0 offen")
+    for i in range(4):
+        st.raw(f"v_add_u32 {T[4 + i]}, 0x4000, {KOFF[i]}")
+    st.nop(1)
+    for i in range(4):
+        st.raw(f"buffer_load_dwordx4 {R('v', 144 + 4 * i, 4)}, {T[4 + i]}, {SK}, 0 offen")
+    # stage 0 = K(2), V(1): the staging descriptors start at tiles 2 / 1
+    st.raw(f"s_add_u32 s40, s40, 0x8000")
+    st.raw(f"s_addc_u32 s41, s41, 0")
+    st.raw(f"s_sub_i32 {SKREM}, s42, 0x8000")
+    st.raw(f"s_max_i32 s42, {SKREM}, 0")
+    st.raw(f"s_add_u32 s44, s44, 0x4000")
+    st.raw(f"s_addc_u32 s45, s45, 0")
+    st.raw(f"s_sub_i32 {SVREM}, s46, 0x4000")
+    st.raw(f"s_max_i32 s46, {SVREM}, 0")
+    st.nop(4)
+    for ins in stage_loads():
+        st.emit(ins)
+    # O, l, -m_ref, m_ref = 0 while the loads fly
+    for x in range(144):
+        st.raw(f"v_accvgpr_write_b32 a{x}, 0")
+    for x in range(96, 112):
+        st.raw(f"v_mov_b32 v{x}, 0")
+    for b in range(4):
+        st.raw(f"v_mov_b32 {MREF[b]}, 0")
+    st.raw("s_waitcnt vmcnt(8)")
+    for i in range(4):
+        st.raw(f"ds_write_b128 %[klds], {R('v', 112 + 4 * i, 4)} offset:{KBUF[0] + 4096 * i}")
+        st.raw(f"ds_write_b128 %[vlds], {R('v', 128 + 4 * i, 4)} offset:{VBUF[0] + 4096 * i}")
+        st.raw(f"ds_write_b128 %[klds], {R('v', 144 + 4 * i, 4)} offset:{KBUF[1] + 4096 * i}")
+    # Q * c (fp32 product, rounded to fp16 once: M16::scale_q), into AGPRs
+    for x in range(64):
+        st.raw(f"v_cvt_f32_f16_e32 {T[0]}, v{x}")
+        st.raw(f"v_cvt_f32_f16_sdwa {T[1]}, v{x} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1")
+        st.raw(f"v_mul_f32_e32 {T[0]}, %[c], {T[0]}")
+        st.raw(f"v_mul_f32_e32 {T[1]}, %[c], {T[1]}")
+        st.raw(f"v_cvt_pk_f16_f32 {T[2]}, {T[0]}, {T[1]}")
+        st.raw(f"v_accvgpr_write_b32 a{144 + x}, {T[2]}")
+    st.raw("s_waitcnt lgkmcnt(0)")
+    st.raw("s_barrier")
+    st.nop(2)
+    st.pos += 0
+    # S(0)
+    qk_plain(st, KBUF[0])
+    st.raw(f"s_cmp_eq_u32 {SMASKJ}, 1")
+    skip = newlabel("nomask0")
+    st.branch("s_cbranch_scc0", skip)
+    st.raw(f"s_sub_i32 {ST0}, %[kvhi], 1")
+    st.raw(f"s_mov_b32 {ST1}, %[qw]")
+    mask_last_tile(st, causal)
+    st.label(skip)
+    slow_softmax(st, first=True)
+    for e in exp_ops():
+        st.emit(e)
+    st.lgkm_all()
+    st.raw("s_barrier")
+    st.raw(f"s_mov_b32 {SJ}, 0")
+
+
+def epilogue(st):
+    """O / l -> fp16 rows (M16::store_o: permlane16 swaps, dwordx4 stores, sc1)"""
+    for b in range(4):
+        l, inv = T[0], T[1]
+        st.emit(valu(f"v_accvgpr_read_b32 {l}, {L(b, 0)}", r=[L(b, 0)], w=[l]))
+        # inv = l > 0 ? 1.0f / l : 0  (IEEE division, the compiler's sequence)
+        st.emit(valu(f"v_div_scale_f32 {T[2]}, s[58:59], {l}, {l}, 1.0", r=[l], w=[T[2]]))
+        st.emit(valu(f"v_rcp_f32_e32 {T[3]}, {T[2]}", r=[T[2]], w=[T[3]]))
+        st.emit(valu(f"v_fma_f32 {T[4]}, -{T[2]}, {T[3]}, 1.0", r=[T[2], T[3]], w=[T[4]]))
+        st.emit(valu(f"v_fmac_f32_e32 {T[3]}, {T[4]}, {T[3]}", r=[T[3], T[4]], w=[T[3]]))
+        st.emit(valu(f"v_div_scale_f32 {T[4]}, vcc, 1.0, {l}, 1.0", r=[l], w=[T[4]]))
+        st.emit(valu(f"v_mul_f32_e32 {T[5]}, {T[4]}, {T[3]}", r=[T[4], T[3]], w=[T[5]]))
+        st.emit(valu(f"v_fma_f32 {T[6]}, -{T[2]}, {T[5]}, {T[4]}", r=[T[2], T[5], T[4]], w=[T[6]]))
+        st.emit(valu(f"v_fmac_f32_e32 {T[5]}, {T[6]}, {T[3]}", r=[T[5], T[6], T[3]], w=[T[5]]))
+        st.emit(valu(f"v_fma_f32 {T[2]}, -{T[2]}, {T[5]}, {T[4]}", r=[T[2], T[5], T[4]], w=[T[2]]))
+        st.emit(valu(f"v_div_fmas_f32 {T[2]}, {T[2]}, {T[3]}, {T[5]}", r=[T[2], T[3], T[5]], w=[T[2]]))
+        st.emit(valu(f"v_div_fixup_f32 {T[2]}, {T[2]}, {l}, 1.0", r=[T[2], l], w=[T[2]]))
+        st.emit(valu(f"v_cmp_lt_f32 vcc, 0, {l}", r=[l]))
+        st.emit(valu(f"v_cndmask_b32 {inv}, 0, {T[2]}, vcc", r=[T[2]], w=[inv]))
+        # row offset: (qw + 16b + r16) * 256 + 2 * dlane
+        st.emit(valu(f"v_add_u32 {T[7]}, {ST1}, %[ooff]", r=["%[ooff]"], w=[T[7]]))
+        if b:
+            st.emit(valu(f"v_add_u32 {T[7]}, {4096 * b}, {T[7]}", r=[T[7]], w=[T[7]]))
+        for ep in range(4):
+            d = [f"v{128 + i}" for i in range(8)]  # O staging: the (free) K fragment slots
+            for x in range(2):
+                e = 2 * ep + x
+                for i in range(4):
+                    src = L(b, i) if DIAG == "l" else O(b, e, i)
+                    st.emit(valu(f"v_accvgpr_read_b32 {d[4 * x + i]}, {src}", r=[src], w=[d[4 * x + i]]))
+                if DIAG in ("raw", "l"):
+                    continue
+                for i in range(4):
+                    st.emit(valu(f"v_mul_f32_e32 {d[4 * x + i]}, {d[4 * x + i]}, {inv}", r=[d[4 * x + i], inv], w=[d[4 * x + i]]))
+            # X = e even pair -> v120,121 ; Y = e odd -> v122,123
+            X, Y = ["v120", "v121"], ["v122", "v123"]
+            st.emit(valu(f"v_cvt_pk_f16_f32 {X[0]}, {d[0]}, {d[1]}", r=d[0:2], w=[X[0]]))
+            st.emit(valu(f"v_cvt_pk_f16_f32 {X[1]}, {d[2]}, {d[3]}", r=d[2:4], w=[X[1]]))
+            st.emit(valu(f"v_cvt_pk_f16_f32 {Y[0]}, {d[4]}, {d[5]}", r=d[4:6], w=[Y[0]]))
+            st.emit(valu(f"v_cvt_pk_f16_f32 {Y[1]}, {d[6]}, {d[7]}", r=d[6:8], w=[Y[1]]))
+            for dw in range(2):
+                st.emit(valu(f"v_permlane16_swap_b32 {X[dw]}, {Y[dw]}", r=[X[dw], Y[dw]], w=[X[dw], Y[dw]]))
+            st.emit(vmem(f"buffer_store_dwordx4 v[120:123], {T[7]}, %[ro], 0 offen offset:{64 * ep} sc1",
+                         r=["v[120:123]", T[7]]))
+            st.nop(2)
+    st.nop(2)
+
+
+def generate(causal):
+    st = Stream()
+    labels = {k: [newlabel(f"{k}{p}") for p in range(2)]
+              for k in ("loop", "notsteady", "masked", "slow", "slow2", "end")}
+    labels["done"] = newlabel("done")
+    prologue(st, causal)
+    # ST1 = qw * 256 for the epilogue (row base), kept in ST1 after the loop
+    body(st, 0, causal, labels)
+    body(st, 1, causal, labels)
+    st.label(labels["done"], drain_lgkm=True)
+    st.raw(f"s_lshl_b32 {ST1}, %[qw], 8")
+    st.nop(1)
+    epilogue(st)
+    return st.out
+
+
+HEADER = """// GENERATED by gen_w4_item.py -- do not edit.
+// One item (256 query rows x all key tiles) of the one-wave-per-SIMD kernel:
+// see the generator's docstring for the register map and the schedule.
+#pragma once
+"""
+
+
+def cxx(causal, lines):
+    body = "\n".join(f'      "{l}\\n"' for l in lines)
+    vclob = ", ".join(f'"v{i}"' for i in range(236))
+    aclob = ", ".join(f'"a{i}"' for i in range(208))
+    sclob = ", ".join(f'"s{i}"' for i in range(40, 60))
+    name = "w4_item_causal" if causal else "w4_item_noncausal"
+    return f"""
+__device__ __forceinline__ void {name}(const W4Item& it, const W4Lane& ln) {{
+  asm volatile(
+{body}
+      :
+      : [rq] "s"(it.rq), [ro] "s"(it.ro),
+        [rk0] "s"(it.rk0), [rk1] "s"(it.rk1), [rk2] "s"(it.rk2), [rk3] "s"(it.rk3),
+        [rv0] "s"(it.rv0), [rv1] "s"(it.rv1), [rv2] "s"(it.rv2), [rv3] "s"(it.rv3),
+        [qw] "s"(it.qw), [ntiles] "s"(it.ntiles), [nw] "s"(it.nw), [masklast] "s"(it.masklast),
+        [kvhi] "s"(it.kvhi), [c] "s"(it.c),
+        [ka0] "v"(ln.ka[0]), [ka1] "v"(ln.ka[1]), [ka2] "v"(ln.ka[2]), [ka3] "v"(ln.ka[3]),
+        [va0] "v"(ln.va[0]), [va1] "v"(ln.va[1]), [koff] "v"(ln.koff), [voff] "v"(ln.voff),
+        [klds] "v"(ln.klds), [vlds] "v"(ln.vlds), [vt] "v"(ln.vt), [r16] "v"(ln.r16),
+        [qoff] "v"(ln.qoff), [ooff] "v"(ln.ooff)
+      : "memory", "vcc", "scc", {sclob},
+        {vclob},
+        {aclob});
+}}
+"""
+
+
+def main():
+    out = sys.argv[1] if len(sys.argv) > 1 else "fa_w4_item.inc"
+    text = HEADER
+    for causal in (False, True):
+        _lbl[0] = 0
+        text += cxx(causal, generate(causal))
+    with open(out, "w") as f:
+        f.write(text)
+
+
+if __name__ == "__main__":
+    main()

@@ -364,6 +364,8 @@ def attention_flops(batch: int, heads: int, seq_len: int, head_dim: int, causal:
 
 def kernel_symbol(config_name: str) -> str:
     """Substring of the kernel symbol rocprofv3 reports for a tile config."""
+    if "_asm_persistent" in config_name:
+        return "fa_fwd_f16_w4_kernel"
     if "persistent" in config_name:
         return "fa_fwd_f16_persistent_kernel"
     if "kvpair" in config_name or "kvquad" in config_name:
