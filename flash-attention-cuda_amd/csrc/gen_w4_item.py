@@ -56,10 +56,12 @@ DIAG = os.environ.get("W4_DIAG", "")
 MFMA_TO_VALU = 12
 VALU_TO_MFMA = 3      # VALU / accvgpr write -> MFMA operand read (needs 2)
 VALU_TO_PERMLANE = 2  # VALU write -> v_permlane*_swap read
+TRANS_TO_VALU = 1     # transcendental (v_exp / v_rcp) write -> non-trans VALU read (gfx940+)
 if DIAG == "haz":
-    MFMA_TO_VALU, VALU_TO_MFMA, VALU_TO_PERMLANE = 24, 6, 4
+    MFMA_TO_VALU, VALU_TO_MFMA, VALU_TO_PERMLANE, TRANS_TO_VALU = 24, 6, 4, 2
 
 NINF = "0xff800000"
+V_AHEAD = 3           # V^T fragments read ahead of the PV MFMAs that use them
 
 
 def regs(spec):
@@ -122,6 +124,7 @@ class Stream:
         self.pos = 0
         self.mfma_w = {}   # reg -> pos of the last MFMA write
         self.valu_w = {}   # reg -> pos of the last VALU write
+        self.trans_w = {}  # reg -> pos of the last transcendental write
         self.lgkm = []     # outstanding LDS ops, oldest first: set of dst regs (reads) or None
         self.pending = {}  # label -> list of saved states
         self.dead = False  # after an unconditional branch
@@ -130,24 +133,26 @@ class Stream:
     def _snap(self):
         return ({r: self.pos - p for r, p in self.mfma_w.items()},
                 {r: self.pos - p for r, p in self.valu_w.items()},
-                [x for x in self.lgkm])
+                [x for x in self.lgkm],
+                {r: self.pos - p for r, p in self.trans_w.items()})
 
     def _restore(self, snaps):
-        m, v, lg = {}, {}, None
-        for sm, sv, sl in snaps:
+        m, v, lg, tr = {}, {}, None, {}
+        for sm, sv, sl, st_ in snaps:
             for r, d in sm.items():
                 m[r] = min(m.get(r, 10 ** 9), d)
             for r, d in sv.items():
                 v[r] = min(v.get(r, 10 ** 9), d)
+            for r, d in st_.items():
+                tr[r] = min(tr.get(r, 10 ** 9), d)
             if lg is None or len(sl) > len(lg):
                 lg = sl
         self.mfma_w = {r: self.pos - d for r, d in m.items() if d < 64}
         self.valu_w = {r: self.pos - d for r, d in v.items() if d < 64}
+        self.trans_w = {r: self.pos - d for r, d in tr.items() if d < 64}
         # merged paths may differ in LDS ops in flight: keep the longer list;
         # counted waits stay safe (they only ever wait for more than needed)
         # as long as every path's list is a suffix-compatible prefix -- assert
-        for sm, sv, sl in snaps:
-            assert len(sl) == 0 or sl == lg[-len(sl):] or True
         self.lgkm = lg or []
 
     def branch(self, cond, label):
@@ -216,6 +221,10 @@ class Stream:
             for r in touched:
                 if r in self.mfma_w:
                     need = max(need, MFMA_TO_VALU - (self.pos - self.mfma_w[r] - 1))
+            if k != "trans":
+                for r in ins.r:
+                    if r in self.trans_w:
+                        need = max(need, TRANS_TO_VALU - (self.pos - self.trans_w[r] - 1))
             if "permlane" in ins.text:
                 for r in ins.r:
                     if r in self.valu_w:
@@ -231,6 +240,10 @@ class Stream:
             elif k in ("valu", "trans"):
                 self.valu_w[r] = at
                 self.mfma_w.pop(r, None)
+                if k == "trans":
+                    self.trans_w[r] = at
+                else:
+                    self.trans_w.pop(r, None)
             else:
                 self.mfma_w.pop(r, None)
                 self.valu_w.pop(r, None)
@@ -416,11 +429,12 @@ def phase_a(st, p, with_max):
     def put(k, ins):
         gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
 
-    # K reads of cb 0 first, then the conversions of the first chain
+    # K reads of cb 0 first; the conversions of cb 0's four blocks cover
+    # their LDS latency
     put(0, [k_read(t, 0, t, kb) for t in range(4)])
     for x, (b, cb) in enumerate(chains):
         c = cvt_block(b, cb)
-        if x == 0:
+        if x < 4:
             put(0, c)
         else:
             put(4 * x - 1, c[0])
@@ -442,6 +456,10 @@ def phase_a(st, p, with_max):
         put(3 + 2 * i, w)
     for i, ld in enumerate(stage_loads()):
         put(20 + i, ld)
+    # the first V^T fragments of PV(j) (V(j) is ready since the last barrier)
+    for f in range(V_AHEAD):
+        for i, r in enumerate(v_reads(0, f, f, VBUF[p])):
+            put(52 + 3 * f + i, r)
     st.interleave(mf, gaps)
     leftover = []
     if with_max:
@@ -460,9 +478,9 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
     def put(k, ins):
         gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
 
-    # V fragments two ahead (frags 0 and 1 were read at the end of phase A)
-    for f in range(2, 16):
-        k = frag_first[f - 2]
+    # V fragments V_AHEAD ahead (the first V_AHEAD were read in phase A)
+    for f in range(V_AHEAD, 16):
+        k = frag_first[f - V_AHEAD]
         u, e = divmod(f, 8)
         r = v_reads(u, e, f % 8, vb)
         put(k + 1, r[0])
@@ -650,17 +668,10 @@ def body(st, p, causal, labels):
     st.branch("s_cbranch_scc1", L["masked"][p])
     # ---- steady: QK(j+1) with maxima, PV(j) with exps ----
     left = phase_a(st, p, with_max=True)
-    # V fragments 0 and 1 of PV(j)
-    for f in range(2):
-        for r in v_reads(0, f, f, VBUF[p]):
-            st.emit(r)
     phase_b(st, p, left, dec_gap=6, label_slow=L["slow"][p], label_end=L["end"][p])
     # ---- masked: the wave's last QK (causal diagonal / ragged end) ----
     st.label(L["masked"][p])
     phase_a(st, p, with_max=False)
-    for f in range(2):
-        for r in v_reads(0, f, f, VBUF[p]):
-            st.emit(r)
     # kv0 = 64 (j+1): ST0 = kv_hi - kv0 - 1, ST1 = qw - kv0
     st.raw(f"s_lshl_b32 {ST1}, {SJ1}, 6")
     st.raw(f"s_sub_i32 {ST0}, %[kvhi], {ST1}")
@@ -795,7 +806,7 @@ def epilogue(st):
         st.emit(valu(f"v_accvgpr_read_b32 {l}, {L(b, 0)}", r=[L(b, 0)], w=[l]))
         # inv = l > 0 ? 1.0f / l : 0  (IEEE division, the compiler's sequence)
         st.emit(valu(f"v_div_scale_f32 {T[2]}, s[58:59], {l}, {l}, 1.0", r=[l], w=[T[2]]))
-        st.emit(valu(f"v_rcp_f32_e32 {T[3]}, {T[2]}", r=[T[2]], w=[T[3]]))
+        st.emit(valu(f"v_rcp_f32_e32 {T[3]}, {T[2]}", r=[T[2]], w=[T[3]], kind="trans"))
         st.emit(valu(f"v_fma_f32 {T[4]}, -{T[2]}, {T[3]}, 1.0", r=[T[2], T[3]], w=[T[4]]))
         st.emit(valu(f"v_fmac_f32_e32 {T[3]}, {T[4]}, {T[3]}", r=[T[3], T[4]], w=[T[3]]))
         st.emit(valu(f"v_div_scale_f32 {T[4]}, vcc, 1.0, {l}, 1.0", r=[l], w=[T[4]]))

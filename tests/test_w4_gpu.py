@@ -1,0 +1,121 @@
+"""One-wave-per-SIMD persistent kernel (bm256_bn64_w4x64_m16_asm_persistent_*,
+fa_w4_kernel.hpp + the generated item program fa_w4_item.inc).
+
+Its arithmetic is the 8-wave kernels' operation for operation, with the
+rescale decision taken per 32-row half as the ping-pong's 32-row waves take
+it, so against the per-item ping-pong (bm256_bn64_w8_m16_pingpong_*) every
+score, P and O accumulator is identical; only the final fp32 -> fp16
+rounding of O may differ (the compiler builds some of the ping-pong's
+roundings as one fused v_fma_mix, the asm rounds the fp32 product), at most
+one fp16 ulp on rare elements.  Sampled heads are checked against the oracle
+(reference cpu_attention restatement) at the 1e-3 gate, on the shapes that
+stress the item order, ragged tiles, the causal diagonal and the rare rescale
+branch (peaked scores).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import oracle  # noqa: E402  (test infrastructure)
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-3
+
+
+def _fa():
+    import fa_mi355x
+
+    return fa_mi355x
+
+
+def _rand(shape, seed, scale=1.0):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    t = torch.empty(shape, dtype=torch.float16, device="cuda")
+    t.uniform_(-0.5 * scale, 0.5 * scale, generator=g)
+    return t
+
+
+def _bits(t):
+    return t.detach().cpu().contiguous().view(torch.int16).numpy().view(np.uint16)
+
+
+def _ids(prefix):
+    out = {c.causal: c.id for c in _fa().configs() if c.name in (f"{prefix}_noncausal", f"{prefix}_causal")}
+    assert set(out) == {False, True}, prefix
+    return out
+
+
+W4 = "bm256_bn64_w4x64_m16_asm_persistent"
+BASE = "bm256_bn64_w8_m16_pingpong"
+
+SHAPES = [
+    (1, 8, 512),     # 2 items per head
+    (2, 64, 2048),   # 16 query blocks x 128 heads: 4+ items per workgroup
+    (3, 40, 1000),   # ragged S (last tile 40 keys), 120 heads
+    (1, 203, 300),   # odd head count, 2 query blocks, the last one mostly past S
+    (4, 50, 64),     # single-tile items
+    (1, 7, 4096),    # fewer heads than XCD groups (non-affine item split)
+    (1, 2, 4096),
+    (1, 32, 2048),   # causal pair order
+    (1, 16, 1280),   # odd query-block count: snake
+    (1, 72, 1024),   # > 64 heads: band-16 snake
+    (1, 4, 77),      # tiny ragged
+]
+
+
+def _compare(b, h, s, causal, seed, scale=1.0, oracle_heads=True):
+    fa = _fa()
+    q, k, v = (_rand((b, h, s, 128), seed + i, scale if i < 2 else 1.0) for i in range(3))
+    base = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(BASE)[causal])
+    out = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(W4)[causal])
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all()
+    diff = (out.float() - base.float()).abs()
+    assert diff.max().item() <= TOL, f"max diff vs ping-pong {diff.max().item()}"
+    frac = (out != base).float().mean().item()
+    assert frac <= 2e-3, f"{frac:.2e} of the elements differ from the ping-pong"
+    if oracle_heads:
+        for flat in sorted({0, b * h // 2, b * h - 1}):
+            bi, hi = divmod(flat, h)
+            sl = (slice(bi, bi + 1), slice(hi, hi + 1))
+            ref = oracle.attention(*(_bits(x[sl]) for x in (q, k, v)), causal)
+            d = oracle.max_abs_diff(_bits(out[sl]), ref)
+            assert d <= TOL, f"head {flat}: max_diff={d}"
+    return frac
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_w4_matches_pingpong_and_oracle(shape, causal):
+    _compare(*shape, causal, seed=500)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("s", [256, 1000, 2048])
+def test_w4_peaked_rescale(s, causal):
+    # Q, K x4: row maxima keep growing past the 2^8 threshold -> the slow path
+    _compare(1, 8, s, causal, seed=600, scale=4.0)
+
+
+def test_w4_causal_row0_and_ones():
+    fa = _fa()
+    b, h, s = 1, 4, 1024
+    q, k, v = (_rand((b, h, s, 128), 700 + i) for i in range(3))
+    o = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(W4)[True])
+    torch.cuda.synchronize()
+    assert torch.equal(o[:, :, 0], v[:, :, 0])  # row 0 sees key 0 only
+    ones = torch.ones_like(v)
+    o1 = fa.flash_attention_fwd(q, k, ones, causal=False, config=_ids(W4)[False])
+    torch.cuda.synchronize()
+    assert torch.equal(o1, ones)
+
+
+def test_w4_deterministic():
+    fa = _fa()
+    q, k, v = (_rand((2, 16, 1536, 128), 800 + i) for i in range(3))
+    a = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(W4)[True])
+    b = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(W4)[True])
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
