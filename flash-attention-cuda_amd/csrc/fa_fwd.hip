@@ -344,7 +344,7 @@ struct Config {
 template <int W, int BN_, int C, int KIND, int SCHED, int DT, int HDIM>
 constexpr kernel_fn pick_kernel() {
   if constexpr (KIND == 5)
-    return fa_fwd_f16_w4_kernel<(C != 0)>;
+    return fa_fwd_f16_w4_kernel<(C != 0), DT == 1>;
   else if constexpr (KIND == 3)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
   else if constexpr (KIND == 4)
@@ -380,9 +380,9 @@ constexpr kernel_fn pick_kernel() {
    pick_kernel<8, 64, C, 4, 1, DT, HDIM>()}
 
 // W4: 4 waves x 64 query rows (one wave per SIMD), K/V double-buffered (64 KB)
-#define FA_CFG_W4(ID, C, NAME)                                                         \
-  {{ID, 256, 64, 4, C, 0, 4 * 64 * ROW_BYTES, NAME, 0, 128}, 0, 5,                      \
-   pick_kernel<4, 64, C, 5, 0, 0, 128>()}
+#define FA_CFG_W4(ID, C, DT, NAME)                                                     \
+  {{ID, 256, 64, 4, C, 0, 4 * 64 * ROW_BYTES, NAME, DT, 128}, 0, 5,                     \
+   pick_kernel<4, 64, C, 5, 0, DT, 128>()}
 
 // Only tiers the dispatcher picks, explicit entry points (split-KV) and the
 // baselines a test compares against (the per-item ping-pong 2/3: the
@@ -432,8 +432,10 @@ static const Config kConfigs[] = {
     FA_CFG_KVQUAD(36, 0, 1, 64, "bf16_d64_bm64_bn64_w8_m16_kvquad_noncausal"),
     FA_CFG_KVQUAD(37, 1, 1, 64, "bf16_d64_bm64_bn64_w8_m16_kvquad_causal"),
     // 4 waves x 64 query rows, persistent, asm item program (fa_w4_kernel.hpp)
-    FA_CFG_W4(38, 0, "bm256_bn64_w4x64_m16_asm_persistent_noncausal"),
-    FA_CFG_W4(39, 1, "bm256_bn64_w4x64_m16_asm_persistent_causal"),
+    FA_CFG_W4(38, 0, 0, "bm256_bn64_w4x64_m16_asm_persistent_noncausal"),
+    FA_CFG_W4(39, 1, 0, "bm256_bn64_w4x64_m16_asm_persistent_causal"),
+    FA_CFG_W4(40, 0, 1, "bf16_bm256_bn64_w4x64_m16_asm_persistent_noncausal"),
+    FA_CFG_W4(41, 1, 1, "bf16_bm256_bn64_w4x64_m16_asm_persistent_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -608,7 +610,15 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
   // non-causal: from 160 items (B=1 H=24 S=2048: 829 vs KV-pair 668; H=6
   // S=8192: 1039 vs 854; at 128 items the KV-pair still wins, 732 vs 532)
   const bool persist = causal ? (wg256 >= 384 || (wg256 >= 256 && nqb256 <= 2)) : wg256 >= 160;
-  if (persist) return cfg_for(256, 8, 64, c, 1, 2);
+  if (persist) {
+    // the one-wave-per-SIMD asm kernel (W4, same items and order), except a
+    // non-causal launch whose last round is short: the ping-pong runs that
+    // tail as KV-pair halves on twice the CUs, W4 has no tail split
+    const long long per_xcd = (wg256 + 7) / 8, cus = std::min<long long>(32, per_xcd);
+    const long long tail = per_xcd % cus;
+    if (!causal && tail > 0 && 2 * tail <= cus) return cfg_for(256, 8, 64, c, 1, 2);
+    return cfg_for(256, 4, 64, c, 0, 5);
+  }
   if (seq_len <= 256) return cfg_for(128, 4, 64, c, 0, 0);
   // causal, two rounds of 64-row blocks over long heads (>= 32 blocks per
   // head): the KV-quad's four-way key split halves the heaviest block's key
@@ -629,7 +639,11 @@ static int launch_auto(int dtype, const void* q, const void* k, const void* v, v
   int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
   if (rc != FA_OK) return rc;
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
-  const int id = twin(fa_select_config(batch, heads, seq_len, causal), dtype, head_dim);
+  const int sel = fa_select_config(batch, heads, seq_len, causal);
+  int id = twin(sel, dtype, head_dim);
+  // W4 is head_dim 128 only: head_dim 64 runs the ping-pong persistent twin
+  if (id < 0 && sel >= 0 && kConfigs[sel].kind == 5)
+    id = twin(cfg_for(256, 8, 64, causal ? 1 : 0, 1, 2), dtype, head_dim);
   if (id < 0) return FA_ERR_BAD_CONFIG;
   return launch(id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
                 (hipStream_t)hip_stream);

@@ -46,6 +46,10 @@ import sys
 # unnormalised), l (store the row sums l in every column), haz (double every
 # hazard window)
 DIAG = os.environ.get("W4_DIAG", "")
+# timing-only experiment switches for diagnostic builds (wrong results):
+# nostage (no K/V staging in phase A), nomax (no running maxima), tmajor
+# (QK^T chains interleaved t-major within a key block)
+XP = set(os.environ.get("W4_XP", "").split(",")) - {""}
 
 # Wait states = instructions issued BETWEEN producer and consumer (s_nop N
 # counts N+1), as LLVM's hazard recognizer counts them.  Required after a
@@ -61,6 +65,18 @@ if DIAG == "haz":
     MFMA_TO_VALU, VALU_TO_MFMA, VALU_TO_PERMLANE, TRANS_TO_VALU = 24, 6, 4, 2
 
 NINF = "0xff800000"
+
+# element type of Q/K/V/O and the MFMA operands (set per generated function):
+# fp16 (the reference's type) or bf16 -- only the MFMA opcode, the fp32 <->
+# 16-bit conversions and the 1.0 constant differ
+DT = {"mfma": "v_mfma_f32_16x16x32_f16", "cvt_pk": "v_cvt_pk_f16_f32", "one2": "0x3c003c00"}
+
+
+def set_dtype(bf16):
+    DT.update({"mfma": "v_mfma_f32_16x16x32_bf16", "cvt_pk": "v_cvt_pk_bf16_f32", "one2": "0x3f803f80"}
+              if bf16 else {"mfma": "v_mfma_f32_16x16x32_f16", "cvt_pk": "v_cvt_pk_f16_f32",
+                            "one2": "0x3c003c00"})
+    DT["bf16"] = bf16
 V_AHEAD = 3           # V^T fragments read ahead of the PV MFMAs that use them
 
 
@@ -90,7 +106,7 @@ class Ins:
 
 
 def mfma(d, a, b, c):
-    return Ins(f"v_mfma_f32_16x16x32_f16 {d}, {a}, {b}, {c}", "mfma", r=[a, b, c] if c[0] in "va" else [a, b], w=[d])
+    return Ins(f"{DT['mfma']} {d}, {a}, {b}, {c}", "mfma", r=[a, b, c] if c[0] in "va" else [a, b], w=[d])
 
 
 def valu(text, r=(), w=(), kind="valu"):
@@ -357,8 +373,8 @@ def cvt_block(b, cb):
     """fp16 P from the exp2'd scores of block (b, cb): pf[b][cb>>1][4(cb&1)+i]"""
     p = 64 + 8 * b + 4 * (cb >> 1) + 2 * (cb & 1)
     s = 16 * b + 4 * cb
-    return [valu(f"v_cvt_pk_f16_f32 v{p}, v{s}, v{s + 1}", r=[f"v{s}", f"v{s + 1}"], w=[f"v{p}"]),
-            valu(f"v_cvt_pk_f16_f32 v{p + 1}, v{s + 2}, v{s + 3}", r=[f"v{s + 2}", f"v{s + 3}"], w=[f"v{p + 1}"])]
+    return [valu(f"{DT['cvt_pk']} v{p}, v{s}, v{s + 1}", r=[f"v{s}", f"v{s + 1}"], w=[f"v{p}"]),
+            valu(f"{DT['cvt_pk']} v{p + 1}, v{s + 2}, v{s + 3}", r=[f"v{s + 2}", f"v{s + 3}"], w=[f"v{p + 1}"])]
 
 
 def max_block(b, cb, first):
@@ -390,22 +406,39 @@ def pv_mfmas():
     return ms, frag_first
 
 
+# Staging sets: stage j's K/V rows live in set j & 1 between their global
+# loads and their LDS writes -- set 0 in VGPRs, set 1 in AGPRs a208-a239 --
+# so the loads of stage j+1 (phase A) and the LDS writes of stage j (phase
+# B) sit in different halves of an iteration.
+STAGE2 = "stage1" not in XP
+
+
+def kst(i, st_set):
+    return KST(i) if st_set == 0 else R("a", 208 + 4 * i, 4)
+
+
+def vst(i, st_set):
+    return VST(i) if st_set == 0 else R("a", 224 + 4 * i, 4)
+
+
 def stage_writes(p):
-    """LDS writes of stage j (K(j+2) -> kbuf[j&1], V(j+1) -> vbuf[(j+1)&1])"""
-    out = ["s_waitcnt vmcnt(0)"]
+    """LDS writes of stage j (K(j+2) -> kbuf[j&1], V(j+1) -> vbuf[(j+1)&1]);
+    with two sets the 8 youngest loads (stage j+1) may still be in flight"""
+    ss = p if STAGE2 else 0
+    out = [f"s_waitcnt vmcnt({8 if STAGE2 else 0})"]
     for i in range(4):
-        out.append(dsw(f"ds_write_b128 %[klds], {KST(i)} offset:{KBUF[p] + 4096 * i}", "%[klds]", KST(i)))
-        out.append(dsw(f"ds_write_b128 %[vlds], {VST(i)} offset:{VBUF[1 - p] + 4096 * i}", "%[vlds]", VST(i)))
+        out.append(dsw(f"ds_write_b128 %[klds], {kst(i, ss)} offset:{KBUF[p] + 4096 * i}", "%[klds]", kst(i, ss)))
+        out.append(dsw(f"ds_write_b128 %[vlds], {vst(i, ss)} offset:{VBUF[1 - p] + 4096 * i}", "%[vlds]", vst(i, ss)))
     return out
 
 
-def stage_loads():
-    """global loads of the next stage into the staging registers, then the
+def stage_loads(st_set=0):
+    """global loads of the next stage into a staging set, then the
     descriptors advance one tile (bytes left clamp at 0: no traffic past the end)"""
     out = []
     for i in range(4):
-        out.append(vmem(f"buffer_load_dwordx4 {KST(i)}, {KOFF[i]}, {SK}, 0 offen", r=[KOFF[i]], w=[KST(i)]))
-        out.append(vmem(f"buffer_load_dwordx4 {VST(i)}, {VOFF[i]}, {SV}, 0 offen", r=[VOFF[i]], w=[VST(i)]))
+        out.append(vmem(f"buffer_load_dwordx4 {kst(i, st_set)}, {KOFF[i]}, {SK}, 0 offen", r=[KOFF[i]], w=[kst(i, st_set)]))
+        out.append(vmem(f"buffer_load_dwordx4 {vst(i, st_set)}, {VOFF[i]}, {SV}, 0 offen", r=[VOFF[i]], w=[vst(i, st_set)]))
     out += [salu("s_add_u32 s40, s40, 0x4000"), salu("s_addc_u32 s41, s41, 0"),
             salu(f"s_sub_i32 {SKREM}, {SKREM}, 0x4000"), salu(f"s_max_i32 s42, {SKREM}, 0"),
             salu("s_add_u32 s44, s44, 0x4000"), salu("s_addc_u32 s45, s45, 0"),
@@ -421,9 +454,16 @@ def phase_a(st, p, with_max):
     kb = KBUF[1 - p]
     chains = [(b, cb) for cb in range(4) for b in range(4)]
     mf = []
-    for x, (b, cb) in enumerate(chains):
-        slots = [4 * (cb & 1) + t for t in range(4)]
-        mf += qk_chain(b, cb, slots)
+    if "tmajor" in XP:
+        for cb in range(4):
+            slots = [4 * (cb & 1) + t for t in range(4)]
+            ch = [qk_chain(b, cb, slots) for b in range(4)]
+            for t in range(4):
+                mf += [ch[b][t] for b in range(4)]
+    else:
+        for x, (b, cb) in enumerate(chains):
+            slots = [4 * (cb & 1) + t for t in range(4)]
+            mf += qk_chain(b, cb, slots)
     gaps = {}
 
     def put(k, ins):
@@ -434,8 +474,11 @@ def phase_a(st, p, with_max):
     put(0, [k_read(t, 0, t, kb) for t in range(4)])
     for x, (b, cb) in enumerate(chains):
         c = cvt_block(b, cb)
-        if x < 4:
-            put(0, c)
+        if x < 4 or ("tmajor" in XP and b > 0):
+            put(4 * (x - b) if x >= 4 else 0, c)
+        elif "tmajor" in XP:
+            put(4 * x - 2, c[0])
+            put(4 * x - 1, c[1])
         else:
             put(4 * x - 1, c[0])
             put(4 * x, c[1])
@@ -443,26 +486,30 @@ def phase_a(st, p, with_max):
         if b == 0 and cb < 3:
             for t in range(4):
                 put(4 * x + 1 + t % 3, k_read(t, cb + 1, 4 * ((cb + 1) & 1) + t, kb))
-        if with_max and x >= 2:
+        if with_max and x >= 2 and "nomax" not in XP:
             y = x - 2
             by, cby = chains[y]
             mm = max_block(by, cby, first=(cby == 0 and by in (0, 2)))
             put(4 * x + 1, mm[0])
             put(4 * x + 2, mm[1])
     # stage traffic: LDS writes in cb 0, loads in cb 1
-    sw = stage_writes(p)
-    put(0, sw[:1])
-    for i, w in enumerate(sw[1:]):
-        put(3 + 2 * i, w)
-    for i, ld in enumerate(stage_loads()):
-        put(20 + i, ld)
+    if "nostage" not in XP and STAGE2:
+        for i, ld in enumerate(stage_loads(1 - p)):
+            put(18 + 2 * i, ld)
+    if "nostage" not in XP and "stage_a" in XP and not STAGE2:
+        sw = stage_writes(p)
+        put(0, sw[:1])
+        for i, w in enumerate(sw[1:]):
+            put(3 + 2 * i, w)
+        for i, ld in enumerate(stage_loads()):
+            put(20 + i, ld)
     # the first V^T fragments of PV(j) (V(j) is ready since the last barrier)
     for f in range(V_AHEAD):
         for i, r in enumerate(v_reads(0, f, f, VBUF[p])):
             put(52 + 3 * f + i, r)
     st.interleave(mf, gaps)
     leftover = []
-    if with_max:
+    if with_max and "nomax" not in XP:
         for y in (14, 15):
             by, cby = chains[y]
             leftover += max_block(by, cby, first=False)
@@ -487,6 +534,16 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
         put(k + 2, r[1])
     for i, ins in enumerate(leftover):
         put(1 + i, ins)
+    # stage traffic (phase A is the denser half): LDS writes of stage j, then
+    # the next stage's global loads, spread over the gaps after the decision
+    if "nostage" not in XP and ("stage_a" not in XP or STAGE2):
+        sw = stage_writes(p)
+        put(dec_gap + 2, sw[:1])
+        for i, w in enumerate(sw[1:]):
+            put(dec_gap + 3 + (6 if STAGE2 else 3) * i, w)
+        if not STAGE2:
+            for i, ld in enumerate(stage_loads()):
+                put(dec_gap + 28 + 2 * i, ld)
     dec = [valu(f"v_max_f32 {T[0]}, {RMAX[0]}, {RMAX[1]}", r=[RMAX[0], RMAX[1]], w=[T[0]]),
            valu(f"v_cmp_lt_f32 vcc, 0x41000000, {T[0]}", r=[T[0]])]
     if exps:
@@ -514,13 +571,18 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
         st.emit(f)
     if not exps:
         return mf, gaps
+    if dec_gap > 0:
+        stamp(st, 60)
+        stamp_acc(st, 65, 60, 62)
+        if DIAG == "stamps":
+            st.raw("s_add_u32 s67, s67, 1")
     st.branch("s_branch", label_end)
     # slow path: the remaining PV MFMAs (no exps), then rescale
     st.label(label_slow)
     for k in range(dec_gap, len(mf)):
         if k > dec_gap:
             for f in gaps.get(k, []):
-                if f.kind != "trans":
+                if isinstance(f, str) or f.kind != "trans":
                     st.emit(f)
         st.emit(mf[k])
     slow_softmax(st, first=False)
@@ -569,6 +631,20 @@ def shift_block(st, b, sh, first):
 
 
 _lbl = [0]
+
+
+def stamp(st, dst):
+    """diagnostic (W4_DIAG=stamps): shader-cycle counter into s[dst:dst+1]"""
+    if DIAG == "stamps":
+        st.raw(f"s_memtime s[{dst}:{dst + 1}]")
+        st.raw("s_waitcnt lgkmcnt(0)")
+        st.lgkm = []
+
+
+def stamp_acc(st, acc, later, earlier):
+    if DIAG == "stamps":
+        st.raw(f"s_sub_u32 s68, s{later}, s{earlier}")
+        st.raw(f"s_add_u32 s{acc}, s{acc}, s68")
 
 
 def newlabel(tag):
@@ -660,6 +736,7 @@ def body(st, p, causal, labels):
     """one loop iteration j of parity p = j & 1"""
     L = labels
     st.label(L["loop"][p], drain_lgkm=True)
+    stamp(st, 60)
     st.raw(f"s_add_u32 {SJ1}, {SJ}, 1")
     st.raw(f"s_cmp_lt_u32 {SJ1}, {SNW}")
     st.branch("s_cbranch_scc0", L["notsteady"][p])
@@ -668,6 +745,8 @@ def body(st, p, causal, labels):
     st.branch("s_cbranch_scc1", L["masked"][p])
     # ---- steady: QK(j+1) with maxima, PV(j) with exps ----
     left = phase_a(st, p, with_max=True)
+    stamp(st, 62)
+    stamp_acc(st, 64, 62, 60)
     phase_b(st, p, left, dec_gap=6, label_slow=L["slow"][p], label_end=L["end"][p])
     # ---- masked: the wave's last QK (causal diagonal / ragged end) ----
     st.label(L["masked"][p])
@@ -682,10 +761,12 @@ def body(st, p, causal, labels):
     phase_b(st, p, [], dec_gap=0, label_slow=L["slow2"][p], label_end=L["end"][p])
     # ---- drain (j = n_w - 1: PV only) / idle (j >= n_w: staging only) ----
     st.label(L["notsteady"][p])
-    for ins in stage_writes(p):
-        st.emit(ins)
-    for ins in stage_loads():
-        st.emit(ins)
+    if STAGE2:
+        for ins in stage_loads(1 - p) + stage_writes(p):
+            st.emit(ins)
+    else:
+        for ins in stage_writes(p) + stage_loads():
+            st.emit(ins)
     st.raw(f"s_cmp_lt_u32 {SJ}, {SNW}")
     st.branch("s_cbranch_scc0", L["end"][p])
     for b in range(4):
@@ -695,6 +776,8 @@ def body(st, p, causal, labels):
     pv_plain(st, p)
     st.label(L["end"][p], drain_lgkm=True)
     st.raw("s_barrier")
+    stamp(st, 62)
+    stamp_acc(st, 66, 62, 60)
     st.raw(f"s_add_u32 {SJ}, {SJ}, 1")
     st.raw(f"s_cmp_lt_u32 {SJ}, %[ntiles]")
     if p == 0:
@@ -722,7 +805,7 @@ def prologue(st, causal):
     st.nop(4)  # SALU-written descriptors -> buffer loads below
     st.raw(f"v_mov_b32 {VNINF}, {NINF}")
     for i in range(4):
-        st.raw(f"v_mov_b32 v{208 + i}, 0x3c003c00")
+        st.raw(f"v_mov_b32 v{208 + i}, {DT['one2']}")
     for i in range(1, 4):
         st.raw(f"v_add_u32 {KOFF[i]}, {4096 * i}, %[koff]")
         st.raw(f"v_add_u32 {VOFF[i]}, {4096 * i}, %[voff]")
@@ -772,11 +855,15 @@ def prologue(st, causal):
         st.raw(f"ds_write_b128 %[klds], {R('v', 144 + 4 * i, 4)} offset:{KBUF[1] + 4096 * i}")
     # Q * c (fp32 product, rounded to fp16 once: M16::scale_q), into AGPRs
     for x in range(64):
-        st.raw(f"v_cvt_f32_f16_e32 {T[0]}, v{x}")
-        st.raw(f"v_cvt_f32_f16_sdwa {T[1]}, v{x} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1")
+        if DT["bf16"]:  # bf16 -> fp32 is exact: the 16 bits move to the top half
+            st.raw(f"v_lshlrev_b32_e32 {T[0]}, 16, v{x}")
+            st.raw(f"v_and_b32_e32 {T[1]}, 0xffff0000, v{x}")
+        else:
+            st.raw(f"v_cvt_f32_f16_e32 {T[0]}, v{x}")
+            st.raw(f"v_cvt_f32_f16_sdwa {T[1]}, v{x} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1")
         st.raw(f"v_mul_f32_e32 {T[0]}, %[c], {T[0]}")
         st.raw(f"v_mul_f32_e32 {T[1]}, %[c], {T[1]}")
-        st.raw(f"v_cvt_pk_f16_f32 {T[2]}, {T[0]}, {T[1]}")
+        st.raw(f"{DT['cvt_pk']} {T[2]}, {T[0]}, {T[1]}")
         st.raw(f"v_accvgpr_write_b32 a{144 + x}, {T[2]}")
     st.raw("s_waitcnt lgkmcnt(0)")
     st.raw("s_barrier")
@@ -797,6 +884,9 @@ def prologue(st, causal):
     st.lgkm_all()
     st.raw("s_barrier")
     st.raw(f"s_mov_b32 {SJ}, 0")
+    if DIAG == "stamps":
+        for r in range(64, 68):
+            st.raw(f"s_mov_b32 s{r}, 0")
 
 
 def epilogue(st):
@@ -835,10 +925,10 @@ def epilogue(st):
                     st.emit(valu(f"v_mul_f32_e32 {d[4 * x + i]}, {d[4 * x + i]}, {inv}", r=[d[4 * x + i], inv], w=[d[4 * x + i]]))
             # X = e even pair -> v120,121 ; Y = e odd -> v122,123
             X, Y = ["v120", "v121"], ["v122", "v123"]
-            st.emit(valu(f"v_cvt_pk_f16_f32 {X[0]}, {d[0]}, {d[1]}", r=d[0:2], w=[X[0]]))
-            st.emit(valu(f"v_cvt_pk_f16_f32 {X[1]}, {d[2]}, {d[3]}", r=d[2:4], w=[X[1]]))
-            st.emit(valu(f"v_cvt_pk_f16_f32 {Y[0]}, {d[4]}, {d[5]}", r=d[4:6], w=[Y[0]]))
-            st.emit(valu(f"v_cvt_pk_f16_f32 {Y[1]}, {d[6]}, {d[7]}", r=d[6:8], w=[Y[1]]))
+            st.emit(valu(f"{DT['cvt_pk']} {X[0]}, {d[0]}, {d[1]}", r=d[0:2], w=[X[0]]))
+            st.emit(valu(f"{DT['cvt_pk']} {X[1]}, {d[2]}, {d[3]}", r=d[2:4], w=[X[1]]))
+            st.emit(valu(f"{DT['cvt_pk']} {Y[0]}, {d[4]}, {d[5]}", r=d[4:6], w=[Y[0]]))
+            st.emit(valu(f"{DT['cvt_pk']} {Y[1]}, {d[6]}, {d[7]}", r=d[6:8], w=[Y[1]]))
             for dw in range(2):
                 st.emit(valu(f"v_permlane16_swap_b32 {X[dw]}, {Y[dw]}", r=[X[dw], Y[dw]], w=[X[dw], Y[dw]]))
             st.emit(vmem(f"buffer_store_dwordx4 v[120:123], {T[7]}, %[ro], 0 offen offset:{64 * ep} sc1",
@@ -860,6 +950,15 @@ def generate(causal):
     st.raw(f"s_lshl_b32 {ST1}, %[qw], 8")
     st.nop(1)
     epilogue(st)
+    if DIAG == "stamps":
+        # [phase A, phase B, barrier (wait + skew), steady iterations] of
+        # this wave, in O[qw][0:8] (every lane the same 16 bytes)
+        for i, r in enumerate(range(64, 68)):
+            st.raw(f"v_mov_b32 v{120 + i}, s{r}")
+        st.raw(f"v_mov_b32 v124, s{ST1[1:]}")
+        st.nop(2)
+        st.raw("buffer_store_dwordx4 v[120:123], v124, %[ro], 0 offen")
+        st.nop(2)
     return st.out
 
 
@@ -870,12 +969,12 @@ HEADER = """// GENERATED by gen_w4_item.py -- do not edit.
 """
 
 
-def cxx(causal, lines):
+def cxx(causal, bf16, lines):
     body = "\n".join(f'      "{l}\\n"' for l in lines)
     vclob = ", ".join(f'"v{i}"' for i in range(236))
-    aclob = ", ".join(f'"a{i}"' for i in range(208))
-    sclob = ", ".join(f'"s{i}"' for i in range(40, 60))
-    name = "w4_item_causal" if causal else "w4_item_noncausal"
+    aclob = ", ".join(f'"a{i}"' for i in range(240 if STAGE2 else 208))
+    sclob = ", ".join(f'"s{i}"' for i in range(40, 70 if DIAG == "stamps" else 60))
+    name = ("w4_item_causal" if causal else "w4_item_noncausal") + ("_bf16" if bf16 else "_f16")
     return f"""
 __device__ __forceinline__ void {name}(const W4Item& it, const W4Lane& ln) {{
   asm volatile(
@@ -900,9 +999,11 @@ __device__ __forceinline__ void {name}(const W4Item& it, const W4Lane& ln) {{
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else "fa_w4_item.inc"
     text = HEADER
-    for causal in (False, True):
-        _lbl[0] = 0
-        text += cxx(causal, generate(causal))
+    for bf16 in (False, True):
+        set_dtype(bf16)
+        for causal in (False, True):
+            _lbl[0] = 0
+            text += cxx(causal, bf16, generate(causal))
     with open(out, "w") as f:
         f.write(text)
 

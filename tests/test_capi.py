@@ -236,16 +236,27 @@ def test_config_table_ships_only_used_tiers():
                 used |= {pre + base for pre in TWIN_PREFIXES if pre + base in by_name}
     baselines = {"bm256_bn64_w8_m16_pingpong_noncausal", "bm256_bn64_w8_m16_pingpong_causal",
                  "bm256_bn64_w8_m16_pingpong_persistent_dma_noncausal",
-                 "bm256_bn64_w8_m16_pingpong_persistent_dma_causal"}
+                 "bm256_bn64_w8_m16_pingpong_persistent_dma_causal",
+                 # the W4 kernel's same-arithmetic baselines (test_w4_gpu.py), and
+                 # the anchor the head_dim-64 fallback twins are looked up from
+                 "bm256_bn64_w8_m16_pingpong_persistent_causal",
+                 "bf16_bm256_bn64_w8_m16_pingpong_persistent_causal",
+                 "bm256_bn64_w8_m16_pingpong_persistent_noncausal",
+                 "bf16_bm256_bn64_w8_m16_pingpong_persistent_noncausal"}
     explicit = {c.name for c in cfgs if c.split_kv}
-    # the one-wave-per-SIMD asm kernel: under evaluation against the ping-pong
-    explicit |= {c.name for c in cfgs if "_asm_persistent_" in c.name}
+    # head_dim 64 of the asm W4 tier runs the ping-pong persistent twins
+    w4 = {n for n in used if "_asm_persistent_" in n}
+    assert w4, "the W4 tier is dispatched"
+    used |= {pre + "bm256_bn64_w8_m16_pingpong_persistent_" + ("causal" if n.endswith("_causal")
+                                                                else "noncausal")
+             for n in w4 for pre in ("d64_", "bf16_d64_")}
     unused = sorted(set(by_name) - used - baselines - explicit)
     assert not unused, unused
-    # every dispatched fp16 d128 tier has all three twins
+    # every dispatched fp16 d128 tier has all three twins (W4: the bf16 one)
     for name in used:
         if not name.startswith(("bf16_", "d64_")):
-            assert all(pre + name in by_name for pre in TWIN_PREFIXES), name
+            pres = ("bf16_",) if name in w4 else TWIN_PREFIXES
+            assert all(pre + name in by_name for pre in pres), name
 
 
 def test_bf16_configs_and_entry_points():

@@ -42,6 +42,7 @@ def _bits(t):
 
 
 def _ids(prefix):
+    """{causal: config id} of the tier named prefix (fp16, or bf16 with a bf16_ prefix)."""
     out = {c.causal: c.id for c in _fa().configs() if c.name in (f"{prefix}_noncausal", f"{prefix}_causal")}
     assert set(out) == {False, True}, prefix
     return out
@@ -119,3 +120,32 @@ def test_w4_deterministic():
     b = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(W4)[True])
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+BF16_W4 = "bf16_" + W4
+BF16_BASE = "bf16_bm256_bn64_w8_m16_pingpong_persistent"
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", [(1, 8, 512), (3, 40, 1000), (1, 72, 1024), (1, 4, 77)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_w4_bf16_matches_pingpong(shape, causal):
+    """bf16 twin: the same item program on the bf16 MFMA; against the bf16
+    persistent ping-pong the arithmetic is again identical up to O's final
+    rounding (one bf16 ulp = 2^-8 relative, |O| < 0.5 here), and the fp32
+    torch reference bounds both at test_bf16_gpu.py's 5e-3."""
+    fa = _fa()
+    b, h, s = shape
+    q, k, v = (_rand((b, h, s, 128), 900 + i).to(torch.bfloat16) for i in range(3))
+    base = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(BF16_BASE)[causal])
+    out = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(BF16_W4)[causal])
+    torch.cuda.synchronize()
+    assert out.dtype == torch.bfloat16
+    diff = (out.float() - base.float()).abs()
+    assert diff.max().item() <= 2.0 ** -9, diff.max().item()
+    assert (out != base).float().mean().item() <= 2e-3
+    sc = q.float() @ k.float().transpose(-1, -2) / 128 ** 0.5
+    if causal:
+        sc = sc + torch.full((s, s), float("-inf"), device="cuda").triu(1)
+    ref = torch.softmax(sc, -1) @ v.float()
+    assert (out.float() - ref).abs().max().item() <= 5e-3
