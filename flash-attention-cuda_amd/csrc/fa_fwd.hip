@@ -83,7 +83,7 @@ __device__ __forceinline__ void run_tile_loop(const FwdParams& p, int bh, int qb
 }
 
 template <int WAVES, int BN, bool CAUSAL, int SCHED, bool BF16 = false, int HDIM = 128>
-__global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_kernel(FwdParams p) {
+__global__ __launch_bounds__(WAVES * 64, BN == 128 ? 1 : 2) void fa_fwd_f16_kernel(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 #ifdef FA_STAMPS
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
@@ -436,6 +436,8 @@ static const Config kConfigs[] = {
     FA_CFG_W4(39, 1, 0, "bm256_bn64_w4x64_m16_asm_persistent_causal"),
     FA_CFG_W4(40, 0, 1, "bf16_bm256_bn64_w4x64_m16_asm_persistent_noncausal"),
     FA_CFG_W4(41, 1, 1, "bf16_bm256_bn64_w4x64_m16_asm_persistent_causal"),
+    FA_CFG(42, 4, 128, 0, 0, 0, "bm128_bn128_w4_m16_noncausal"),
+    FA_CFG(43, 4, 128, 1, 0, 0, "bm128_bn128_w4_m16_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 

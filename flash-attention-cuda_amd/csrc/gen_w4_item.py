@@ -411,6 +411,10 @@ def pv_mfmas():
 # so the loads of stage j+1 (phase A) and the LDS writes of stage j (phase
 # B) sit in different halves of an iteration.
 STAGE2 = "stage1" not in XP
+# first phase-A gap and spacing of the next stage's global loads (8 loads +
+# 8 descriptor updates)
+LD_AT = int(os.environ.get("W4_LD_AT", "18"))
+LD_SP = int(os.environ.get("W4_LD_SP", "2"))
 
 
 def kst(i, st_set):
@@ -467,14 +471,21 @@ def phase_a(st, p, with_max):
     gaps = {}
 
     def put(k, ins):
-        gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
+        ins = ins if isinstance(ins, list) else [ins]
+        if "nokread" in XP:
+            ins = [i for i in ins if isinstance(i, str) or "ds_read_b128" not in i.text]
+        if "novread" in XP:
+            ins = [i for i in ins if isinstance(i, str) or "ds_read_b64_tr" not in i.text]
+        gaps.setdefault(k, []).extend(ins)
 
     # K reads of cb 0 first; the conversions of cb 0's four blocks cover
     # their LDS latency
     put(0, [k_read(t, 0, t, kb) for t in range(4)])
     for x, (b, cb) in enumerate(chains):
         c = cvt_block(b, cb)
-        if x < 4 or ("tmajor" in XP and b > 0):
+        if "nocvt" in XP:
+            pass
+        elif x < 4 or ("tmajor" in XP and b > 0):
             put(4 * (x - b) if x >= 4 else 0, c)
         elif "tmajor" in XP:
             put(4 * x - 2, c[0])
@@ -482,8 +493,11 @@ def phase_a(st, p, with_max):
         else:
             put(4 * x - 1, c[0])
             put(4 * x, c[1])
-        # next cb's K fragments early in this cb's first chain
-        if b == 0 and cb < 3:
+        # next cb's K fragments early in this cb's first chain (kspread: one
+        # per chain of this cb)
+        if "kspread" in XP and cb < 3:
+            put(4 * x + 1, k_read(b, cb + 1, 4 * ((cb + 1) & 1) + b, kb))
+        elif b == 0 and cb < 3:
             for t in range(4):
                 put(4 * x + 1 + t % 3, k_read(t, cb + 1, 4 * ((cb + 1) & 1) + t, kb))
         if with_max and x >= 2 and "nomax" not in XP:
@@ -495,7 +509,7 @@ def phase_a(st, p, with_max):
     # stage traffic: LDS writes in cb 0, loads in cb 1
     if "nostage" not in XP and STAGE2:
         for i, ld in enumerate(stage_loads(1 - p)):
-            put(18 + 2 * i, ld)
+            put(LD_AT + LD_SP * i, ld)
     if "nostage" not in XP and "stage_a" in XP and not STAGE2:
         sw = stage_writes(p)
         put(0, sw[:1])
@@ -523,7 +537,10 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
     gaps = {}
 
     def put(k, ins):
-        gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
+        ins = ins if isinstance(ins, list) else [ins]
+        if "novread" in XP:
+            ins = [i for i in ins if isinstance(i, str) or "ds_read_b64_tr" not in i.text]
+        gaps.setdefault(k, []).extend(ins)
 
     # V fragments V_AHEAD ahead (the first V_AHEAD were read in phase A)
     for f in range(V_AHEAD, 16):
@@ -544,9 +561,10 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
         if not STAGE2:
             for i, ld in enumerate(stage_loads()):
                 put(dec_gap + 28 + 2 * i, ld)
-    dec = [valu(f"v_max_f32 {T[0]}, {RMAX[0]}, {RMAX[1]}", r=[RMAX[0], RMAX[1]], w=[T[0]]),
+    dec = [valu(f"v_max_f32 {T[0]}, {RMAX[0]}, {RMAX[1]}", r=[RMAX[0], RMAX[1]], w=[T[0]])
+           if "nomax" not in XP else valu(f"v_mov_b32 {T[0]}, 0", w=[T[0]]),
            valu(f"v_cmp_lt_f32 vcc, 0x41000000, {T[0]}", r=[T[0]])]
-    if exps:
+    if exps and "noexp" not in XP:
         ex = exp_ops()
         n_g = len(mf) - dec_gap
         for i, e in enumerate(ex):

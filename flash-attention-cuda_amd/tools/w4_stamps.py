@@ -35,7 +35,7 @@ rows = o.view(torch.int32).view(a.batch, a.heads, a.seq, 64)[:, :, ::64, :4].res
 tot = rows.to(torch.float64).sum(0)
 it = tot[3].item()
 res = {"config": fa.configs()[a.config].name, "seq": a.seq, "batch": a.batch, "causal": a.causal,
-       "steady_iters": it, "cyc_phase_a": tot[0].item() / it, "cyc_phase_b": tot[1].item() / it,
-       "cyc_barrier": tot[2].item() / it}
+       "steady_iters": it, "cyc_phase_a": tot[0].item() / max(it, 1), "cyc_phase_b": tot[1].item() / max(it, 1),
+       "cyc_barrier": tot[2].item() / max(it, 1)}
 res["cyc_tile"] = res["cyc_phase_a"] + res["cyc_phase_b"] + res["cyc_barrier"]
 print(json.dumps({k: (round(v, 1) if isinstance(v, float) else v) for k, v in res.items()}))
