@@ -381,7 +381,7 @@ constexpr kernel_fn pick_kernel() {
 
 // W4: 4 waves x 64 query rows (one wave per SIMD), K/V double-buffered (64 KB)
 #define FA_CFG_W4(ID, C, DT, NAME)                                                     \
-  {{ID, 256, 64, 4, C, 0, 4 * 64 * ROW_BYTES, NAME, DT, 128}, 0, 5,                     \
+  {{ID, 256, 64, 4, C, 0, kW4LdsBytes, NAME, DT, 128}, 0, 5,                             \
    pick_kernel<4, 64, C, 5, 0, DT, 128>()}
 
 // Only tiers the dispatcher picks, explicit entry points (split-KV) and the
@@ -678,6 +678,127 @@ extern "C" int fa_fwd_f16(const void* q, const void* k, const void* v, void* o, 
                      hip_stream);
 }
 
+// ---- causal split tier (workspace entries) -----------------------------------
+// Short causal launches (fewer 256-row items than the persistent tier needs):
+// fa_fwd_f16_w4s_kernel cuts each query block's key range into pieces of T
+// 64-key tiles, one workgroup each, merged in-launch through the workspace.
+// T = the shortest piece (>= 4 tiles: the diagonal piece keeps every wave
+// busy) whose pieces all fit one round on the device's CUs, at most 8 pieces
+// per query block.
+struct SplitPlan {
+  int T = 0, pmax = 0, nqb = 0;
+  long long items = 0;
+  unsigned long long ctr_bytes = 0, lse_bytes = 0, o_bytes = 0;
+  unsigned long long bytes() const { return ctr_bytes + lse_bytes + o_bytes; }
+};
+
+static SplitPlan split_plan(int batch, int heads, int seq_len, int head_dim, int causal) {
+  SplitPlan sp;
+  if (!causal || head_dim != HD || batch <= 0 || heads <= 0 || seq_len < 512) return sp;
+  const long long bh = (long long)batch * heads;
+  const int nqb = (seq_len + 255) / 256;
+  const long long wg256 = bh * nqb;
+  if (wg256 >= 384 || (wg256 >= 256 && nqb <= 2)) return sp;  // the persistent tier's shapes
+  const long long cus = num_cus();
+  for (int T = 4; T <= 4 * nqb; ++T) {
+    long long items = 0;
+    int pmax = 1;
+    for (int qb = 0; qb < nqb; ++qb) {
+      const int tiles = (std::min(256 * (qb + 1), seq_len) + 63) / 64;
+      const int np = (tiles + T - 1) / T;
+      items += bh * np;
+      pmax = std::max(pmax, np);
+    }
+    if (items <= cus && pmax <= 8) {
+      if (pmax == 1) return sp;  // nothing to split
+      sp.T = T;
+      sp.pmax = pmax;
+      sp.nqb = nqb;
+      sp.items = items;
+      sp.ctr_bytes = ((unsigned long long)bh * nqb * 4 + 255) / 256 * 256;
+      sp.lse_bytes = (unsigned long long)bh * nqb * pmax * 256 * 4;
+      sp.o_bytes = (unsigned long long)bh * nqb * pmax * 256 * ROW_BYTES;
+      return sp;
+    }
+  }
+  return sp;
+}
+
+template <bool BF16>
+static int launch_split(const SplitPlan& sp, const void* q, const void* k, const void* v, void* o,
+                        int bh, int seq_len, void* ws, hipStream_t stream) {
+  constexpr int kLds = 4 * 64 * ROW_BYTES;
+  static std::once_flag flags[64];
+  static hipError_t errs[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return FA_ERR_HIP;
+  std::call_once(flags[dev], [dev] {
+    errs[dev] = hipFuncSetAttribute((const void*)fa_fwd_f16_w4s_kernel<BF16>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+  });
+  if (errs[dev] != hipSuccess) return FA_ERR_HIP;
+  FwdParams p = {};
+  p.q = static_cast<const f16*>(q);
+  p.k = static_cast<const f16*>(k);
+  p.v = static_cast<const f16*>(v);
+  p.o = static_cast<f16*>(o);
+  p.seq_len = seq_len;
+  p.bh = bh;
+  p.nqb = sp.nqb;
+  p.num_splits = 1;
+  p.scale = 1.0f / sqrtf((float)HD);
+  p.c = p.scale * 1.4426950408889634f;
+  p.band = 1;
+  char* w = static_cast<char*>(ws);
+  p.ws_ctr = reinterpret_cast<unsigned*>(w);
+  p.ws_lse = reinterpret_cast<float*>(w + sp.ctr_bytes);
+  p.ws_o = w + sp.ctr_bytes + sp.lse_bytes;
+  p.piece_tiles = sp.T;
+  p.pmax = sp.pmax;
+  hipLaunchKernelGGL(fa_fwd_f16_w4s_kernel<BF16>, dim3((unsigned)sp.items), dim3(256), kLds,
+                     stream, p);
+  return hipGetLastError() == hipSuccess ? FA_OK : FA_ERR_LAUNCH;
+}
+
+static int launch_ws(int dtype, const void* q, const void* k, const void* v, void* o, int batch,
+                     int heads, int seq_len, int head_dim, int causal, void* ws,
+                     unsigned long long ws_bytes, void* hip_stream) {
+  int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
+  if (rc != FA_OK) return rc;
+  if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
+  const SplitPlan sp = split_plan(batch, heads, seq_len, head_dim, causal);
+  if (sp.T == 0)
+    return launch_auto(dtype, q, k, v, o, batch, heads, seq_len, head_dim, causal, hip_stream);
+  if (!ws || ws_bytes < sp.bytes()) return FA_ERR_WORKSPACE;
+  const int bh = batch * heads;
+  return dtype == FA_DTYPE_BF16
+             ? launch_split<true>(sp, q, k, v, o, bh, seq_len, ws, (hipStream_t)hip_stream)
+             : launch_split<false>(sp, q, k, v, o, bh, seq_len, ws, (hipStream_t)hip_stream);
+}
+
+extern "C" unsigned long long fa_fwd_ws_bytes(int batch, int heads, int seq_len, int head_dim,
+                                              int causal) {
+  return split_plan(batch, heads, seq_len, head_dim, causal).bytes();
+}
+
+extern "C" int fa_fwd_split_pieces(int batch, int heads, int seq_len, int head_dim, int causal) {
+  return split_plan(batch, heads, seq_len, head_dim, causal).T;
+}
+
+extern "C" int fa_fwd_f16_ws(const void* q, const void* k, const void* v, void* o, int batch,
+                             int heads, int seq_len, int head_dim, int causal, void* workspace,
+                             unsigned long long ws_bytes, void* hip_stream) {
+  return launch_ws(FA_DTYPE_F16, q, k, v, o, batch, heads, seq_len, head_dim, causal, workspace,
+                   ws_bytes, hip_stream);
+}
+
+extern "C" int fa_fwd_bf16_ws(const void* q, const void* k, const void* v, void* o, int batch,
+                              int heads, int seq_len, int head_dim, int causal, void* workspace,
+                              unsigned long long ws_bytes, void* hip_stream) {
+  return launch_ws(FA_DTYPE_BF16, q, k, v, o, batch, heads, seq_len, head_dim, causal, workspace,
+                   ws_bytes, hip_stream);
+}
+
 // ---- split-KV ---------------------------------------------------------------
 static int splitkv_cfg(int causal) { return cfg_for(128, 4, 64, causal ? 1 : 0, 0, 1); }
 
@@ -772,7 +893,7 @@ extern "C" const char* fa_status_string(int status) {
     case FA_ERR_LAUNCH: return "kernel launch failed";
     case FA_ERR_BAD_CONFIG: return "bad tile config";
     case FA_ERR_HIP: return "HIP runtime error";
-    case FA_ERR_WORKSPACE: return "split-KV buffers missing";
+    case FA_ERR_WORKSPACE: return "split-KV buffers or workspace missing or too small";
     default: return "unknown status";
   }
 }

@@ -81,6 +81,14 @@ struct FwdParams {
   float c;         // scale * log2(e)
   float scale;     // 1/sqrt(head_dim)
   int band;        // causal: query blocks of one head kept together on an XCD
+  // causal split tier (fa_fwd_*_ws, fa_w4_kernel.hpp): the workspace's
+  // arrival counters [bh][nqb], per-row log2-sum-exp and normalised partial
+  // O slabs [bh][nqb][pmax][256 rows], and the 64-key tiles per key piece
+  unsigned* ws_ctr;
+  float* ws_lse;
+  char* ws_o;
+  int piece_tiles;
+  int pmax;
 };
 
 // ---------------------------------------------------------------------------

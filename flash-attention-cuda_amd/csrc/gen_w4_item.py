@@ -333,7 +333,8 @@ def Q(b, t):
 
 
 # LDS: K buffers at 0 / 16384, V buffers at 32768 / 49152 (lane addresses
-# carry the workgroup's LDS base)
+# carry the workgroup's LDS base); the next item's Q rows (LDS-DMA) at
+# 65536 + 16384 * wave (%[qlw], %[qrd])
 KBUF = [0, 16384]
 VBUF = [32768, 49152]
 KADDR = [f"%[ka{t}]" for t in range(4)]
@@ -773,7 +774,7 @@ def body(st, p, causal, labels):
     st.raw(f"s_lshl_b32 {ST1}, {SJ1}, 6")
     st.raw(f"s_sub_i32 {ST0}, %[kvhi], {ST1}")
     st.raw(f"s_sub_i32 {ST0}, {ST0}, 1")
-    st.raw(f"s_sub_i32 {ST1}, %[qw], {ST1}")
+    st.raw(f"s_sub_i32 {ST1}, %[qm], {ST1}")
     mask_last_tile(st, causal)
     full_max(st)
     phase_b(st, p, [], dec_gap=0, label_slow=L["slow2"][p], label_end=L["end"][p])
@@ -785,6 +786,27 @@ def body(st, p, causal, labels):
     else:
         for ins in stage_writes(p) + stage_loads():
             st.emit(ins)
+    # the item's last iteration (j + 1 == ntiles) with a next item
+    # (%[flags] bit 0): prefetch its Q, K(0), K(1) (both K images are dead)
+    # (between the MFMAs of the PV drain where this wave has one)
+    nodma, idle = newlabel("nodma"), newlabel("dmaidle")
+    st.raw(f"s_cmp_eq_u32 {SJ1}, %[ntiles]")
+    st.branch("s_cbranch_scc0", nodma)
+    st.raw("s_bitcmp1_b32 %[flags], 0")
+    st.branch("s_cbranch_scc0", nodma)
+    st.raw("s_waitcnt lgkmcnt(0)")  # this wave's last stage writes land before its DMA pieces
+    st.raw(f"s_cmp_lt_u32 {SJ}, {SNW}")
+    st.branch("s_cbranch_scc0", idle)
+    for b in range(4):
+        for cb in range(4):
+            for c in cvt_block(b, cb):
+                st.emit(c)
+    pv_dma(st, p)
+    st.branch("s_branch", L["end"][p])
+    st.label(idle)
+    next_dma(st)
+    st.branch("s_branch", L["end"][p])
+    st.label(nodma)
     st.raw(f"s_cmp_lt_u32 {SJ}, {SNW}")
     st.branch("s_cbranch_scc0", L["end"][p])
     for b in range(4):
@@ -804,9 +826,129 @@ def body(st, p, causal, labels):
         st.branch("s_cbranch_scc1", L["loop"][0])
 
 
+def pstamp(st, dst):
+    """diagnostic (W4_DIAG=pstamps): shader-cycle counter into s[dst:dst+1]"""
+    if DIAG == "pstamps":
+        st.raw(f"s_memtime s[{dst}:{dst + 1}]")
+        st.raw("s_waitcnt lgkmcnt(0)")
+        st.lgkm = []
+
+
+def next_dma_groups():
+    """the next item's LDS-DMA pieces (see next_dma) as instruction groups,
+    to be placed between MFMAs; s39 keeps m0, ST0 = qwn * 256 (set first)"""
+    groups = []
+    for i in range(16):
+        b, t = divmod(i, 4)
+        groups.append([f"s_add_u32 {ST1}, {ST0}, {4096 * b + 64 * t}",
+                       f"s_add_u32 m0, %[qlw], {1024 * i}", "s_nop 0",
+                       f"buffer_load_dwordx4 %[qoff], %[rqn], {ST1} offen lds"])
+    for kt in range(2):
+        for i in range(4):
+            groups.append([f"s_mov_b32 {ST1}, {16384 * kt + 4096 * i}",
+                           f"s_add_u32 m0, %[kdw], {KBUF[kt] + 4096 * i}", "s_nop 0",
+                           f"buffer_load_dwordx4 %[kdma], %[rkn], {ST1} offen lds"])
+    return groups
+
+
+def pv_dma(st, p):
+    """pv_plain with the next item's DMA pieces in every third MFMA gap"""
+    vb = VBUF[p]
+    mf, frag_first = pv_mfmas()
+    gaps = {}
+    for f in range(16):
+        u, e = divmod(f, 8)
+        k = frag_first[f - 2] + 1 if f >= 2 else 0
+        for i, r in enumerate(v_reads(u, e, f % 8, vb)):
+            gaps.setdefault(k + i if f >= 2 else 0, []).append(r)
+    st.raw("s_mov_b32 s39, m0")
+    st.raw(f"s_lshl_b32 {ST0}, %[qwn], 8")
+    for g, grp in enumerate(next_dma_groups()):
+        gaps.setdefault(2 + 3 * g, []).extend(grp)
+    st.interleave(mf, gaps)
+    st.raw("s_mov_b32 m0, s39")
+
+
+def next_dma(st):
+    """LDS-DMA (buffer_load ... lds) of the NEXT item's operands, issued in
+    this item's last iteration once both K images are dead: this wave's 64 Q
+    rows into its QBUF region (lane-linear: piece 4b+t holds what the cold
+    prologue's load (b, t) puts in v[16b+4t]) and its quarter of K(0), K(1)
+    into KBUF 0/1 (the source chunk per lane chosen so the lane-linear write
+    lands in the k_off16 image).  The next item's prologue then loads only
+    V(0) and stage 0 from memory."""
+    st.raw("s_mov_b32 s39, m0")
+    st.raw(f"s_lshl_b32 {ST0}, %[qwn], 8")
+    for i in range(16):
+        b, t = divmod(i, 4)
+        st.raw(f"s_add_u32 {ST1}, {ST0}, {4096 * b + 64 * t}")
+        st.raw(f"s_add_u32 m0, %[qlw], {1024 * i}")
+        st.raw("s_nop 0")
+        st.raw(f"buffer_load_dwordx4 %[qoff], %[rqn], {ST1} offen lds")
+    for kt in range(2):
+        for i in range(4):
+            st.raw(f"s_mov_b32 {ST1}, {16384 * kt + 4096 * i}")
+            st.raw(f"s_add_u32 m0, %[kdw], {KBUF[kt] + 4096 * i}")
+            st.raw("s_nop 0")
+            st.raw(f"buffer_load_dwordx4 %[kdma], %[rkn], {ST1} offen lds")
+    st.raw("s_mov_b32 m0, s39")
+
+
+def stage0(st):
+    """staging descriptors start at tiles K(2) / V(1); stage 0's loads"""
+    st.raw(f"s_add_u32 s40, s40, 0x8000")
+    st.raw(f"s_addc_u32 s41, s41, 0")
+    st.raw(f"s_sub_i32 {SKREM}, s42, 0x8000")
+    st.raw(f"s_max_i32 s42, {SKREM}, 0")
+    st.raw(f"s_add_u32 s44, s44, 0x4000")
+    st.raw(f"s_addc_u32 s45, s45, 0")
+    st.raw(f"s_sub_i32 {SVREM}, s46, 0x4000")
+    st.raw(f"s_max_i32 s46, {SVREM}, 0")
+    st.nop(4)
+    for ins in stage_loads():
+        st.emit(ins)
+
+
+def zero_state(st):
+    """O, l, -m_ref, m_ref = 0"""
+    for x in range(144):
+        st.raw(f"v_accvgpr_write_b32 a{x}, 0")
+    for x in range(96, 112):
+        st.raw(f"v_mov_b32 v{x}, 0")
+    for b in range(4):
+        st.raw(f"v_mov_b32 {MREF[b]}, 0")
+
+
+def q_scale(st):
+    """Q * c (fp32 product, rounded to fp16 once: M16::scale_q) from v0-63
+    into AGPRs, eight elements at a time in the (free) V^T fragment registers"""
+    for x0 in range(0, 64, 8):
+        xs = range(x0, x0 + 8)
+        lo = {x: f"v{144 + 3 * (x - x0)}" for x in xs}
+        hi = {x: f"v{145 + 3 * (x - x0)}" for x in xs}
+        pk = {x: f"v{146 + 3 * (x - x0)}" for x in xs}
+        for x in xs:
+            if DT["bf16"]:  # bf16 -> fp32 is exact: the 16 bits move to the top half
+                st.raw(f"v_lshlrev_b32_e32 {lo[x]}, 16, v{x}")
+                st.raw(f"v_and_b32_e32 {hi[x]}, 0xffff0000, v{x}")
+            else:
+                st.raw(f"v_cvt_f32_f16_e32 {lo[x]}, v{x}")
+                st.raw(f"v_cvt_f32_f16_sdwa {hi[x]}, v{x} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1")
+        for x in xs:
+            st.raw(f"v_mul_f32_e32 {lo[x]}, %[c], {lo[x]}")
+            st.raw(f"v_mul_f32_e32 {hi[x]}, %[c], {hi[x]}")
+        for x in xs:
+            st.raw(f"{DT['cvt_pk']} {pk[x]}, {lo[x]}, {hi[x]}")
+        for x in xs:
+            st.raw(f"v_accvgpr_write_b32 a{144 + x}, {pk[x]}")
+
+
 def prologue(st, causal):
     """Q (scaled), K(0), K(1), V(0) into registers / LDS, stage 0 in flight,
-    S(0) = K(0) Q^T with the first-tile rescale and exp2"""
+    S(0) = K(0) Q^T with the first-tile rescale and exp2.  Cold (the
+    workgroup's first item): everything from memory.  Warm (%[flags] bit 1):
+    Q, K(0), K(1) arrived by LDS-DMA during the previous item (next_dma)."""
+    pstamp(st, 60)
     st.raw("s_mov_b32 s40, %[rk0]")
     st.raw("s_mov_b32 s41, %[rk1]")
     st.raw("s_mov_b32 s42, %[rk2]")
@@ -827,6 +969,10 @@ def prologue(st, causal):
     for i in range(1, 4):
         st.raw(f"v_add_u32 {KOFF[i]}, {4096 * i}, %[koff]")
         st.raw(f"v_add_u32 {VOFF[i]}, {4096 * i}, %[voff]")
+    warm, join = newlabel("warm"), newlabel("join")
+    st.raw("s_bitcmp1_b32 %[flags], 1")
+    st.branch("s_cbranch_scc1", warm)
+    # ---- cold ----
     # Q rows qw + 16b + r16: offset (qw + 16b) * 256 + %[qoff]
     st.raw(f"s_lshl_b32 {ST0}, %[qw], 8")
     for b in range(4):
@@ -837,78 +983,86 @@ def prologue(st, causal):
     for b in range(4):
         for t in range(4):
             st.raw(f"buffer_load_dwordx4 {R('v', 16 * b + 4 * t, 4)}, {T[b]}, %[rq], 0 offen offset:{64 * t}")
-    # K(0) -> v112.., V(0) -> v128.., K(1) -> v144.. (tile offsets in VGPR temps)
+    # K(0) -> v112.., then V(0) and K(1) into staging set 1 (a224.., a208..:
+    # free until iteration 0's loads), waited for only after S(0)
     for i in range(4):
         st.raw(f"buffer_load_dwordx4 {R('v', 112 + 4 * i, 4)}, {KOFF[i]}, {SK}, 0 offen")
     for i in range(4):
-        st.raw(f"buffer_load_dwordx4 {R('v', 128 + 4 * i, 4)}, {VOFF[i]}, {SV}, 0 offen")
+        st.raw(f"buffer_load_dwordx4 {vst(i, 1)}, {VOFF[i]}, {SV}, 0 offen")
     for i in range(4):
         st.raw(f"v_add_u32 {T[4 + i]}, 0x4000, {KOFF[i]}")
     st.nop(1)
     for i in range(4):
-        st.raw(f"buffer_load_dwordx4 {R('v', 144 + 4 * i, 4)}, {T[4 + i]}, {SK}, 0 offen")
-    # stage 0 = K(2), V(1): the staging descriptors start at tiles 2 / 1
-    st.raw(f"s_add_u32 s40, s40, 0x8000")
-    st.raw(f"s_addc_u32 s41, s41, 0")
-    st.raw(f"s_sub_i32 {SKREM}, s42, 0x8000")
-    st.raw(f"s_max_i32 s42, {SKREM}, 0")
-    st.raw(f"s_add_u32 s44, s44, 0x4000")
-    st.raw(f"s_addc_u32 s45, s45, 0")
-    st.raw(f"s_sub_i32 {SVREM}, s46, 0x4000")
-    st.raw(f"s_max_i32 s46, {SVREM}, 0")
-    st.nop(4)
-    for ins in stage_loads():
-        st.emit(ins)
-    # O, l, -m_ref, m_ref = 0 while the loads fly
-    for x in range(144):
-        st.raw(f"v_accvgpr_write_b32 a{x}, 0")
-    for x in range(96, 112):
-        st.raw(f"v_mov_b32 v{x}, 0")
-    for b in range(4):
-        st.raw(f"v_mov_b32 {MREF[b]}, 0")
-    st.raw("s_waitcnt vmcnt(8)")
+        st.raw(f"buffer_load_dwordx4 {kst(i, 1)}, {T[4 + i]}, {SK}, 0 offen")
+    stage0(st)
+    zero_state(st)
+    # Q and K(0) landed (V(0), K(1) and stage 0 may still fly)
+    st.raw("s_waitcnt vmcnt(16)")
     for i in range(4):
         st.raw(f"ds_write_b128 %[klds], {R('v', 112 + 4 * i, 4)} offset:{KBUF[0] + 4096 * i}")
-        st.raw(f"ds_write_b128 %[vlds], {R('v', 128 + 4 * i, 4)} offset:{VBUF[0] + 4096 * i}")
-        st.raw(f"ds_write_b128 %[klds], {R('v', 144 + 4 * i, 4)} offset:{KBUF[1] + 4096 * i}")
-    # Q * c (fp32 product, rounded to fp16 once: M16::scale_q), into AGPRs
-    for x in range(64):
-        if DT["bf16"]:  # bf16 -> fp32 is exact: the 16 bits move to the top half
-            st.raw(f"v_lshlrev_b32_e32 {T[0]}, 16, v{x}")
-            st.raw(f"v_and_b32_e32 {T[1]}, 0xffff0000, v{x}")
-        else:
-            st.raw(f"v_cvt_f32_f16_e32 {T[0]}, v{x}")
-            st.raw(f"v_cvt_f32_f16_sdwa {T[1]}, v{x} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1")
-        st.raw(f"v_mul_f32_e32 {T[0]}, %[c], {T[0]}")
-        st.raw(f"v_mul_f32_e32 {T[1]}, %[c], {T[1]}")
-        st.raw(f"{DT['cvt_pk']} {T[2]}, {T[0]}, {T[1]}")
-        st.raw(f"v_accvgpr_write_b32 a{144 + x}, {T[2]}")
+    q_scale(st)
     st.raw("s_waitcnt lgkmcnt(0)")
     st.raw("s_barrier")
+    st.branch("s_branch", join)
+    # ---- warm ----
+    st.label(warm)
+    # the DMA pieces (older than the previous item's 16 O stores) landed,
+    # in every wave
+    st.raw("s_waitcnt vmcnt(16)")
+    st.raw("s_barrier")
+    for i in range(16):
+        b, t = divmod(i, 4)
+        st.raw(f"ds_read_b128 {R('v', 16 * b + 4 * t, 4)}, %[qrd] offset:{1024 * i}")
+    for i in range(4):
+        st.raw(f"buffer_load_dwordx4 {vst(i, 1)}, {VOFF[i]}, {SV}, 0 offen")
+    stage0(st)
+    zero_state(st)
+    st.raw("s_waitcnt lgkmcnt(0)")
+    q_scale(st)
+    st.label(join)
     st.nop(2)
-    st.pos += 0
     # S(0)
     qk_plain(st, KBUF[0])
     st.raw(f"s_cmp_eq_u32 {SMASKJ}, 1")
     skip = newlabel("nomask0")
     st.branch("s_cbranch_scc0", skip)
     st.raw(f"s_sub_i32 {ST0}, %[kvhi], 1")
-    st.raw(f"s_mov_b32 {ST1}, %[qw]")
+    st.raw(f"s_mov_b32 {ST1}, %[qm]")
     mask_last_tile(st, causal)
     st.label(skip)
     slow_softmax(st, first=True)
     for e in exp_ops():
         st.emit(e)
-    st.lgkm_all()
+    # V(0) (and on the cold path K(1)) landed: into their LDS images
+    st.raw("s_waitcnt vmcnt(8)")
+    for i in range(4):
+        st.raw(f"ds_write_b128 %[vlds], {vst(i, 1)} offset:{VBUF[0] + 4096 * i}")
+    nok1 = newlabel("nok1")
+    st.raw("s_bitcmp1_b32 %[flags], 1")
+    st.branch("s_cbranch_scc1", nok1)
+    for i in range(4):
+        st.raw(f"ds_write_b128 %[klds], {kst(i, 1)} offset:{KBUF[1] + 4096 * i}")
+    st.label(nok1)
+    st.raw("s_waitcnt lgkmcnt(0)")
+    st.lgkm = []
     st.raw("s_barrier")
+    pstamp(st, 62)
     st.raw(f"s_mov_b32 {SJ}, 0")
     if DIAG == "stamps":
         for r in range(64, 68):
             st.raw(f"s_mov_b32 s{r}, 0")
 
 
-def epilogue(st):
-    """O / l -> fp16 rows (M16::store_o: permlane16 swaps, dwordx4 stores, sc1)"""
+def epilogue(st, split):
+    """O / l -> fp16 rows (M16::store_o: permlane16 swaps, dwordx4 stores, sc1).
+    split: the item is one key piece of its query block -- the normalised
+    partial O goes to the workspace slab (%[ro] points there) and the row's
+    log2-sum-exp, m_ref + log2(l), to %[rl] (4-B sc1 stores), for the merge"""
+    if split:
+        st.raw(f"s_lshl_b32 s57, %[qw], 2")
+        st.nop(1)
+        st.emit(valu(f"v_lshlrev_b32 {T[9]}, 2, %[r16]", r=["%[r16]"], w=[T[9]]))
+        st.emit(valu(f"v_add_u32 {T[9]}, s57, {T[9]}", r=[T[9]], w=[T[9]]))
     for b in range(4):
         l, inv = T[0], T[1]
         st.emit(valu(f"v_accvgpr_read_b32 {l}, {L(b, 0)}", r=[L(b, 0)], w=[l]))
@@ -926,6 +1080,13 @@ def epilogue(st):
         st.emit(valu(f"v_div_fixup_f32 {T[2]}, {T[2]}, {l}, 1.0", r=[T[2], l], w=[T[2]]))
         st.emit(valu(f"v_cmp_lt_f32 vcc, 0, {l}", r=[l]))
         st.emit(valu(f"v_cndmask_b32 {inv}, 0, {T[2]}, vcc", r=[T[2]], w=[inv]))
+        if split:
+            # log2(l) + m_ref (-inf for an empty row), row qw + 16b + r16
+            st.emit(valu(f"v_log_f32_e32 {T[8]}, {l}", r=[l], w=[T[8]], kind="trans"))
+            st.emit(valu(f"v_add_f32_e32 {T[8]}, {MREF[b]}, {T[8]}", r=[MREF[b], T[8]], w=[T[8]]))
+            st.emit(valu(f"v_add_u32 {T[10]}, {64 * b}, {T[9]}", r=[T[9]], w=[T[10]]))
+            st.emit(vmem(f"buffer_store_dword {T[8]}, {T[10]}, %[rl], 0 offen sc1", r=[T[8], T[10]]))
+            st.nop(2)
         # row offset: (qw + 16b + r16) * 256 + 2 * dlane
         st.emit(valu(f"v_add_u32 {T[7]}, {ST1}, %[ooff]", r=["%[ooff]"], w=[T[7]]))
         if b:
@@ -955,7 +1116,7 @@ def epilogue(st):
     st.nop(2)
 
 
-def generate(causal):
+def generate(causal, split=False):
     st = Stream()
     labels = {k: [newlabel(f"{k}{p}") for p in range(2)]
               for k in ("loop", "notsteady", "masked", "slow", "slow2", "end")}
@@ -965,9 +1126,23 @@ def generate(causal):
     body(st, 0, causal, labels)
     body(st, 1, causal, labels)
     st.label(labels["done"], drain_lgkm=True)
+    pstamp(st, 64)
     st.raw(f"s_lshl_b32 {ST1}, %[qw], 8")
     st.nop(1)
-    epilogue(st)
+    epilogue(st, split)
+    if DIAG == "pstamps":
+        # [prologue, loop, epilogue issue, store drain] cycles of this wave's
+        # item, in O[qw][0:8] (every lane the same 16 bytes)
+        pstamp(st, 66)
+        st.raw("s_waitcnt vmcnt(0)")
+        pstamp(st, 68)
+        for i, (a, b) in enumerate(((62, 60), (64, 62), (66, 64), (68, 66))):
+            st.raw(f"s_sub_u32 s57, s{a}, s{b}")
+            st.raw(f"v_mov_b32 v{120 + i}, s57")
+        st.raw(f"v_mov_b32 v124, s{ST1[1:]}")
+        st.nop(2)
+        st.raw("buffer_store_dwordx4 v[120:123], v124, %[ro], 0 offen")
+        st.nop(2)
     if DIAG == "stamps":
         # [phase A, phase B, barrier (wait + skew), steady iterations] of
         # this wave, in O[qw][0:8] (every lane the same 16 bytes)
@@ -987,12 +1162,13 @@ HEADER = """// GENERATED by gen_w4_item.py -- do not edit.
 """
 
 
-def cxx(causal, bf16, lines):
+def cxx(causal, bf16, lines, split=False):
     body = "\n".join(f'      "{l}\\n"' for l in lines)
     vclob = ", ".join(f'"v{i}"' for i in range(236))
     aclob = ", ".join(f'"a{i}"' for i in range(240 if STAGE2 else 208))
-    sclob = ", ".join(f'"s{i}"' for i in range(40, 70 if DIAG == "stamps" else 60))
-    name = ("w4_item_causal" if causal else "w4_item_noncausal") + ("_bf16" if bf16 else "_f16")
+    sclob = ", ".join(f'"s{i}"' for i in range(39, 70 if DIAG in ("stamps", "pstamps") else 60))
+    name = (("w4_item_causal" if causal else "w4_item_noncausal") + ("_split" if split else "")
+            + ("_bf16" if bf16 else "_f16"))
     return f"""
 __device__ __forceinline__ void {name}(const W4Item& it, const W4Lane& ln) {{
   asm volatile(
@@ -1001,12 +1177,14 @@ __device__ __forceinline__ void {name}(const W4Item& it, const W4Lane& ln) {{
       : [rq] "s"(it.rq), [ro] "s"(it.ro),
         [rk0] "s"(it.rk0), [rk1] "s"(it.rk1), [rk2] "s"(it.rk2), [rk3] "s"(it.rk3),
         [rv0] "s"(it.rv0), [rv1] "s"(it.rv1), [rv2] "s"(it.rv2), [rv3] "s"(it.rv3),
-        [qw] "s"(it.qw), [ntiles] "s"(it.ntiles), [nw] "s"(it.nw), [masklast] "s"(it.masklast),
+        [qw] "s"(it.qw), [qm] "s"(it.qm), [rl] "s"(it.rl),
+        [rqn] "s"(it.rqn), [rkn] "s"(it.rkn), [qwn] "s"(it.qwn), [flags] "s"(it.flags),
+        [qlw] "s"(it.qlw), [kdw] "s"(it.kdw), [ntiles] "s"(it.ntiles), [nw] "s"(it.nw), [masklast] "s"(it.masklast),
         [kvhi] "s"(it.kvhi), [c] "s"(it.c),
         [ka0] "v"(ln.ka[0]), [ka1] "v"(ln.ka[1]), [ka2] "v"(ln.ka[2]), [ka3] "v"(ln.ka[3]),
         [va0] "v"(ln.va[0]), [va1] "v"(ln.va[1]), [koff] "v"(ln.koff), [voff] "v"(ln.voff),
         [klds] "v"(ln.klds), [vlds] "v"(ln.vlds), [vt] "v"(ln.vt), [r16] "v"(ln.r16),
-        [qoff] "v"(ln.qoff), [ooff] "v"(ln.ooff)
+        [qoff] "v"(ln.qoff), [ooff] "v"(ln.ooff), [qrd] "v"(ln.qrd), [kdma] "v"(ln.kdma)
       : "memory", "vcc", "scc", {sclob},
         {vclob},
         {aclob});
@@ -1022,6 +1200,9 @@ def main():
         for causal in (False, True):
             _lbl[0] = 0
             text += cxx(causal, bf16, generate(causal))
+        # one key piece of a causal query block (fa_w4_kernel.hpp: split tier)
+        _lbl[0] = 0
+        text += cxx(True, bf16, generate(True, split=True), split=True)
     with open(out, "w") as f:
         f.write(text)
 

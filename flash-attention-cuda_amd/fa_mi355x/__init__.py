@@ -42,6 +42,10 @@ EXPORTED_SYMBOLS = (
     "fa_splitkv_num_splits",
     "fa_splitkv_o_bytes",
     "fa_splitkv_ml_bytes",
+    "fa_fwd_f16_ws",
+    "fa_fwd_bf16_ws",
+    "fa_fwd_ws_bytes",
+    "fa_fwd_split_pieces",
     "fa_select_config",
     "fa_num_configs",
     "fa_config_info",
@@ -134,6 +138,14 @@ def load_library() -> ctypes.CDLL:
     lib.fa_splitkv_o_bytes.restype = ull
     lib.fa_splitkv_ml_bytes.argtypes = [i, i, i, i, i]
     lib.fa_splitkv_ml_bytes.restype = ull
+    lib.fa_fwd_f16_ws.argtypes = [vp, vp, vp, vp, i, i, i, i, i, vp, ull, vp]
+    lib.fa_fwd_f16_ws.restype = i
+    lib.fa_fwd_bf16_ws.argtypes = [vp, vp, vp, vp, i, i, i, i, i, vp, ull, vp]
+    lib.fa_fwd_bf16_ws.restype = i
+    lib.fa_fwd_ws_bytes.argtypes = [i, i, i, i, i]
+    lib.fa_fwd_ws_bytes.restype = ull
+    lib.fa_fwd_split_pieces.argtypes = [i, i, i, i, i]
+    lib.fa_fwd_split_pieces.restype = i
     lib.fa_select_config.argtypes = [i, i, i, i]
     lib.fa_select_config.restype = i
     lib.fa_num_configs.argtypes = []
@@ -237,6 +249,42 @@ def _check_qkvo_each(q, k, v, out):
                                       f"{name} is on {t.device}, q on {q.device}: one device only")
 
 
+_WS_NEED = {}  # (device, B, H, S, D, causal) -> workspace bytes (fa_fwd_ws_bytes)
+_WS_BUF = {}   # (device, stream) -> zero-filled uint8 workspace, kept for the process
+
+
+def workspace_bytes(batch: int, heads: int, seq_len: int, head_dim: int, causal: bool,
+                    device=None) -> int:
+    """Workspace the split tier needs for this shape on `device` (0: no split)."""
+    import torch
+
+    dev = torch.cuda.current_device() if device is None else torch.device(device).index
+    key = (dev, batch, heads, seq_len, head_dim, bool(causal))
+    n = _WS_NEED.get(key)
+    if n is None:
+        with torch.cuda.device(dev):
+            n = load_library().fa_fwd_ws_bytes(batch, heads, seq_len, head_dim, int(bool(causal)))
+        _WS_NEED[key] = n
+    return n
+
+
+def _workspace(nbytes: int, dev: int, st: int):
+    """A zero-filled workspace of >= nbytes for launches on stream `st` of
+    device `dev`, from torch's caching allocator, reused by every later launch
+    on that stream (each launch leaves it reusable: fa_mi355x.h).  Under HIP
+    graph capture a fresh one is captured with its zero fill instead."""
+    import torch
+
+    if torch.cuda.is_current_stream_capturing():
+        return torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+    buf = _WS_BUF.get((dev, st))
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        torch.cuda.current_stream(dev).synchronize()  # the fill lands before any stream uses it
+        _WS_BUF[(dev, st)] = buf
+    return buf
+
+
 def flash_attention_fwd(q, k, v, causal: bool = False, out=None, config: Optional[int] = None,
                         stream=None):
     """O = softmax(Q K^T / sqrt(D) [+ causal mask]) V for fp16 or bf16 BHSD tensors.
@@ -244,7 +292,10 @@ def flash_attention_fwd(q, k, v, causal: bool = False, out=None, config: Optiona
     q, k, v: [batch, heads, seq_len, D] float16 (the reference's type) or
     bfloat16 contiguous device tensors, all of one dtype; D = 128 (the
     reference's head_dim) or 64.
-    config: force a tile config id (see :func:`configs`); default = dispatcher.
+    config: force a tile config id (see :func:`configs`); default = dispatcher,
+    which for short causal shapes splits query blocks' key ranges across
+    workgroups through a workspace from torch's caching allocator
+    (fa_fwd_*_ws; :func:`workspace_bytes`).
     Enqueued on ``stream`` (default: torch's current stream); no sync.
     """
     import torch
@@ -262,7 +313,14 @@ def flash_attention_fwd(q, k, v, causal: bool = False, out=None, config: Optiona
         st = stream if isinstance(stream, int) else stream.cuda_stream
     args = (q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), b, h, s, d, int(bool(causal)))
     if config is None:
-        fn = lib.fa_fwd_bf16 if bf16 else lib.fa_fwd_f16
+        need = _WS_NEED.get((dev, b, h, s, d, bool(causal)))
+        if need is None:
+            need = workspace_bytes(b, h, s, d, causal, device=q.device)
+        if need:
+            fn = lib.fa_fwd_bf16_ws if bf16 else lib.fa_fwd_f16_ws
+            args += (_workspace(need, dev, st).data_ptr(), need)
+        else:
+            fn = lib.fa_fwd_bf16 if bf16 else lib.fa_fwd_f16
     else:
         fn = lib.fa_fwd_bf16_config if bf16 else lib.fa_fwd_f16_config
         args += (int(config),)

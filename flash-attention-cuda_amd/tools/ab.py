@@ -48,7 +48,9 @@ for var in a.libs.split(","):
     fa._lib = None
     fa.LIB_PATH = os.path.join(HERE, "lib", "libfa_mi355x%s.so" % ("_" + var if var else ""))
     libs[var] = fa.load_library()
-cids = [(var, int(x)) for x in a.configs.split(",") for var in libs]
+# "auto": the default dispatch (flash_attention_fwd with config=None: the
+# workspace split tier where it applies)
+cids = [(var, None if x == "auto" else int(x)) for x in a.configs.split(",") for var in libs]
 flops = fa.attention_flops(a.batch, a.heads, a.seq, a.head_dim, a.causal)
 res = {c: [] for c in cids}
 for c in cids:  # warm
@@ -67,6 +69,7 @@ for _ in range(a.rounds):
         en.synchronize()
         res[c].append(flops / (st.elapsed_time(en) / a.iters / 1e3) / 1e12)
 names = {c.id: c.name for c in fa.configs()}
+names[None] = "auto(split=%d)" % fa.load_library().fa_fwd_split_pieces(a.batch, a.heads, a.seq, a.head_dim, int(a.causal))
 for c in cids:
     print(json.dumps({"config": names[c[1]], "lib": c[0] or "base", "env": a.env, "seq": a.seq, "head_dim": a.head_dim, "batch": a.batch, "heads": a.heads, "data": a.data, "causal": a.causal,
                       "median_tflops": round(statistics.median(res[c]), 1),

@@ -38,7 +38,7 @@ typedef enum {
   FA_ERR_LAUNCH = 4,              /* hipGetLastError() after the launch */
   FA_ERR_BAD_CONFIG = 5,          /* config id out of range / wrong causal */
   FA_ERR_HIP = 6,                 /* other HIP runtime failure */
-  FA_ERR_WORKSPACE = 7            /* split-KV buffers missing */
+  FA_ERR_WORKSPACE = 7            /* split-KV buffers / workspace missing or short */
 } fa_status_t;
 
 /* Tile configuration descriptor (the reference's template switches
@@ -114,6 +114,29 @@ unsigned long long fa_splitkv_o_bytes(int batch, int heads, int seq_len,
                                       int head_dim, int num_splits);
 unsigned long long fa_splitkv_ml_bytes(int batch, int heads, int seq_len,
                                        int head_dim, int num_splits);
+
+/* Workspace forward: fa_fwd_f16 / fa_fwd_bf16 plus a caller-owned device
+ * workspace that lets short causal launches split each query block's key
+ * range across workgroups and merge the pieces in the same launch (the
+ * reference's split-K LSE merge, :559-598, without a second kernel).
+ * fa_fwd_ws_bytes() is the workspace this shape needs on the current device,
+ * 0 when the dispatcher does not split it (the _ws entries then run exactly
+ * fa_fwd_f16 / fa_fwd_bf16 and ignore the workspace).  The workspace must be
+ * zero-filled before its first use; every launch leaves it reusable (its
+ * arrival counters back at zero), so one buffer serves any number of
+ * launches on ONE stream (launches on different streams need their own).
+ * FA_ERR_WORKSPACE if the shape splits and workspace is NULL or ws_bytes is
+ * short.  fa_fwd_split_pieces() is the key-piece length in 64-key tiles the
+ * dispatcher would use (0 = no split). */
+unsigned long long fa_fwd_ws_bytes(int batch, int heads, int seq_len, int head_dim,
+                                   int causal);
+int fa_fwd_split_pieces(int batch, int heads, int seq_len, int head_dim, int causal);
+int fa_fwd_f16_ws(const void* q, const void* k, const void* v, void* o,
+                  int batch, int heads, int seq_len, int head_dim, int causal,
+                  void* workspace, unsigned long long ws_bytes, void* hip_stream);
+int fa_fwd_bf16_ws(const void* q, const void* k, const void* v, void* o,
+                   int batch, int heads, int seq_len, int head_dim, int causal,
+                   void* workspace, unsigned long long ws_bytes, void* hip_stream);
 
 /* The dispatcher's decision (ref tier table :620-661): config id used by
  * fa_fwd_f16 for this shape. */

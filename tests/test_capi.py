@@ -89,6 +89,8 @@ def test_config_table():
         need = 2 * nbuf * c.block_n * 256
         if "_pingpong_persistent_" in c.name and "_dma_" not in c.name and not c.causal:
             need = max(need, KVPAIR_LDS)  # room for the KV-pair tail halves
+        if "_w4x64_" in c.name:
+            need += 256 * 256  # the next item's Q rows (LDS-DMA prefetch)
         assert c.lds_bytes == need <= 160 * 1024
     # every (waves, bn) non-split config exists for both masks
     nonsplit = {(c.waves, c.block_n, c.causal) for c in cfgs if not c.split_kv}
@@ -288,3 +290,26 @@ def test_bf16_configs_and_entry_points():
                 c = cfgs[fa.select_config(b, h, s, causal)]
                 assert any(t.waves == c.waves and t.causal == c.causal and t.block_m == c.block_m
                            for t in bf), c.name
+
+
+def test_split_plan_and_workspace_entry():
+    """The causal split tier's plan (fa_fwd_split_pieces / fa_fwd_ws_bytes)
+    and the workspace entry's argument checks -- no launch, no GPU needed."""
+    fa = _fa()
+    lib = fa.load_library()
+    # short causal: pieces of >= 4 tiles; B=1 H=32 S=1024 -> 8 pieces of 6 per head
+    t = lib.fa_fwd_split_pieces(1, 32, 1024, 128, 1)
+    assert t >= 4
+    need = lib.fa_fwd_ws_bytes(1, 32, 1024, 128, 1)
+    assert need > 0 and need % 256 == 0
+    # no split: non-causal, head_dim 64, the persistent tier's shapes, S < 512
+    for args in ((1, 32, 1024, 128, 0), (1, 32, 1024, 64, 1), (64, 32, 4096, 128, 1),
+                 (1, 32, 8192, 128, 1), (1, 32, 256, 128, 1)):
+        assert lib.fa_fwd_split_pieces(*args) == 0, args
+        assert lib.fa_fwd_ws_bytes(*args) == 0, args
+    p = ctypes.c_void_p(0x1000)
+    assert lib.fa_fwd_f16_ws(p, p, p, p, 1, 32, 1024, 128, 1, None, need, None) == fa.FA_ERR_WORKSPACE
+    assert lib.fa_fwd_f16_ws(p, p, p, p, 1, 32, 1024, 128, 1, p, need - 1, None) == fa.FA_ERR_WORKSPACE
+    assert lib.fa_fwd_bf16_ws(p, p, p, p, 1, 32, 1024, 96, 1, p, need, None) == \
+        fa.FA_ERR_UNSUPPORTED_HEAD_DIM
+    assert lib.fa_fwd_f16_ws(None, p, p, p, 1, 32, 1024, 128, 1, p, need, None) == fa.FA_ERR_NULL_POINTER
