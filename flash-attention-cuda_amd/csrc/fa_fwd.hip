@@ -692,36 +692,67 @@ struct SplitPlan {
   unsigned long long bytes() const { return ctr_bytes + lse_bytes + o_bytes; }
 };
 
-static SplitPlan split_plan(int batch, int heads, int seq_len, int head_dim, int causal) {
+// Workspace layout: arrival counters in a FIXED first 64 KB (one per query
+// block, at most 16384 blocks), then the per-row log2-sum-exp, then the
+// partial O slabs.  The counter region never overlaps another shape's data
+// regions, so one zero-filled buffer stays valid across shapes: every launch
+// returns the counters it used to zero.
+constexpr unsigned long long kSplitCtrBytes = 65536;
+
+// the plan for piece length T (64-key tiles), or none if a query block would
+// need more than 8 pieces (the merge's limit) or the launch has more query
+// blocks than counters
+static SplitPlan plan_for(long long bh, int seq_len, int T) {
   SplitPlan sp;
-  if (!causal || head_dim != HD || batch <= 0 || heads <= 0 || seq_len < 512) return sp;
+  const int nqb = (seq_len + 255) / 256;
+  if (bh * nqb > (long long)(kSplitCtrBytes / 4)) return sp;
+  long long items = 0;
+  int pmax = 1;
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int tiles = (std::min(256 * (qb + 1), seq_len) + 63) / 64;
+    const int np = (tiles + T - 1) / T;
+    items += bh * np;
+    pmax = std::max(pmax, np);
+  }
+  if (pmax > 8) return sp;
+  sp.T = T;
+  sp.pmax = pmax;
+  sp.nqb = nqb;
+  sp.items = items;
+  sp.ctr_bytes = kSplitCtrBytes;
+  sp.lse_bytes = (unsigned long long)bh * nqb * pmax * 256 * 4;
+  sp.o_bytes = (unsigned long long)bh * nqb * pmax * 256 * ROW_BYTES;
+  return sp;
+}
+
+// piece_tiles > 0: that piece length (causal, head_dim 128; T = 0 if it
+// needs more than 8 pieces); 0: the dispatcher's choice -- long causal
+// launches short of the persistent tier (S >= 4096, fewer than 384 256-row
+// items): the split beats the KV-quad tier there (B=1 H=8 S=4096 662 vs 612
+// TFLOP/s, H=4 S=8192 801 vs 716, H=2 S=16384 923 vs 810, H=4 S=4096 481 vs
+// 414) and loses below S=4096 (H=8 S=2048 303 vs 349, B=1 H=32 S=1024 335
+// vs KV-pair 434: a W4 item's ~11k-cycle prologue and the merge outweigh
+// the balance; profiles/r03_ab_split_tier*.jsonl)
+static SplitPlan split_plan(int batch, int heads, int seq_len, int head_dim, int causal,
+                            int piece_tiles = 0) {
+  SplitPlan none;
+  if (!causal || head_dim != HD || batch <= 0 || heads <= 0 || seq_len <= 0) return none;
   const long long bh = (long long)batch * heads;
+  if (piece_tiles > 0) {
+    SplitPlan sp = plan_for(bh, seq_len, piece_tiles);
+    return sp.pmax > 1 ? sp : none;  // one piece per block: not a split
+  }
   const int nqb = (seq_len + 255) / 256;
   const long long wg256 = bh * nqb;
-  if (wg256 >= 384 || (wg256 >= 256 && nqb <= 2)) return sp;  // the persistent tier's shapes
+  if (seq_len < 4096 || wg256 >= 384) return none;  // short, or the persistent tier's shapes
   const long long cus = num_cus();
+  // the shortest piece (>= 4 tiles: the diagonal piece keeps every wave
+  // busy) whose pieces all fit one round on the device's CUs
   for (int T = 4; T <= 4 * nqb; ++T) {
-    long long items = 0;
-    int pmax = 1;
-    for (int qb = 0; qb < nqb; ++qb) {
-      const int tiles = (std::min(256 * (qb + 1), seq_len) + 63) / 64;
-      const int np = (tiles + T - 1) / T;
-      items += bh * np;
-      pmax = std::max(pmax, np);
-    }
-    if (items <= cus && pmax <= 8) {
-      if (pmax == 1) return sp;  // nothing to split
-      sp.T = T;
-      sp.pmax = pmax;
-      sp.nqb = nqb;
-      sp.items = items;
-      sp.ctr_bytes = ((unsigned long long)bh * nqb * 4 + 255) / 256 * 256;
-      sp.lse_bytes = (unsigned long long)bh * nqb * pmax * 256 * 4;
-      sp.o_bytes = (unsigned long long)bh * nqb * pmax * 256 * ROW_BYTES;
-      return sp;
-    }
+    const SplitPlan sp = plan_for(bh, seq_len, T);
+    if (sp.T && sp.items <= cus) return sp.pmax > 1 ? sp : none;
   }
-  return sp;
+  return none;
 }
 
 template <bool BF16>
@@ -761,12 +792,13 @@ static int launch_split(const SplitPlan& sp, const void* q, const void* k, const
 }
 
 static int launch_ws(int dtype, const void* q, const void* k, const void* v, void* o, int batch,
-                     int heads, int seq_len, int head_dim, int causal, void* ws,
+                     int heads, int seq_len, int head_dim, int causal, int piece_tiles, void* ws,
                      unsigned long long ws_bytes, void* hip_stream) {
   int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
   if (rc != FA_OK) return rc;
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
-  const SplitPlan sp = split_plan(batch, heads, seq_len, head_dim, causal);
+  const SplitPlan sp = split_plan(batch, heads, seq_len, head_dim, causal, piece_tiles);
+  if (piece_tiles > 0 && sp.T == 0) return FA_ERR_BAD_CONFIG;  // not a causal d128 split
   if (sp.T == 0)
     return launch_auto(dtype, q, k, v, o, batch, heads, seq_len, head_dim, causal, hip_stream);
   if (!ws || ws_bytes < sp.bytes()) return FA_ERR_WORKSPACE;
@@ -777,8 +809,8 @@ static int launch_ws(int dtype, const void* q, const void* k, const void* v, voi
 }
 
 extern "C" unsigned long long fa_fwd_ws_bytes(int batch, int heads, int seq_len, int head_dim,
-                                              int causal) {
-  return split_plan(batch, heads, seq_len, head_dim, causal).bytes();
+                                              int causal, int piece_tiles) {
+  return split_plan(batch, heads, seq_len, head_dim, causal, piece_tiles).bytes();
 }
 
 extern "C" int fa_fwd_split_pieces(int batch, int heads, int seq_len, int head_dim, int causal) {
@@ -786,17 +818,17 @@ extern "C" int fa_fwd_split_pieces(int batch, int heads, int seq_len, int head_d
 }
 
 extern "C" int fa_fwd_f16_ws(const void* q, const void* k, const void* v, void* o, int batch,
-                             int heads, int seq_len, int head_dim, int causal, void* workspace,
-                             unsigned long long ws_bytes, void* hip_stream) {
-  return launch_ws(FA_DTYPE_F16, q, k, v, o, batch, heads, seq_len, head_dim, causal, workspace,
-                   ws_bytes, hip_stream);
+                             int heads, int seq_len, int head_dim, int causal, int piece_tiles,
+                             void* workspace, unsigned long long ws_bytes, void* hip_stream) {
+  return launch_ws(FA_DTYPE_F16, q, k, v, o, batch, heads, seq_len, head_dim, causal, piece_tiles,
+                   workspace, ws_bytes, hip_stream);
 }
 
 extern "C" int fa_fwd_bf16_ws(const void* q, const void* k, const void* v, void* o, int batch,
-                              int heads, int seq_len, int head_dim, int causal, void* workspace,
-                              unsigned long long ws_bytes, void* hip_stream) {
-  return launch_ws(FA_DTYPE_BF16, q, k, v, o, batch, heads, seq_len, head_dim, causal, workspace,
-                   ws_bytes, hip_stream);
+                              int heads, int seq_len, int head_dim, int causal, int piece_tiles,
+                              void* workspace, unsigned long long ws_bytes, void* hip_stream) {
+  return launch_ws(FA_DTYPE_BF16, q, k, v, o, batch, heads, seq_len, head_dim, causal, piece_tiles,
+                   workspace, ws_bytes, hip_stream);
 }
 
 // ---- split-KV ---------------------------------------------------------------

@@ -333,8 +333,7 @@ def Q(b, t):
 
 
 # LDS: K buffers at 0 / 16384, V buffers at 32768 / 49152 (lane addresses
-# carry the workgroup's LDS base); the next item's Q rows (LDS-DMA) at
-# 65536 + 16384 * wave (%[qlw], %[qrd])
+# carry the workgroup's LDS base)
 KBUF = [0, 16384]
 VBUF = [32768, 49152]
 KADDR = [f"%[ka{t}]" for t in range(4)]
@@ -786,27 +785,6 @@ def body(st, p, causal, labels):
     else:
         for ins in stage_writes(p) + stage_loads():
             st.emit(ins)
-    # the item's last iteration (j + 1 == ntiles) with a next item
-    # (%[flags] bit 0): prefetch its Q, K(0), K(1) (both K images are dead)
-    # (between the MFMAs of the PV drain where this wave has one)
-    nodma, idle = newlabel("nodma"), newlabel("dmaidle")
-    st.raw(f"s_cmp_eq_u32 {SJ1}, %[ntiles]")
-    st.branch("s_cbranch_scc0", nodma)
-    st.raw("s_bitcmp1_b32 %[flags], 0")
-    st.branch("s_cbranch_scc0", nodma)
-    st.raw("s_waitcnt lgkmcnt(0)")  # this wave's last stage writes land before its DMA pieces
-    st.raw(f"s_cmp_lt_u32 {SJ}, {SNW}")
-    st.branch("s_cbranch_scc0", idle)
-    for b in range(4):
-        for cb in range(4):
-            for c in cvt_block(b, cb):
-                st.emit(c)
-    pv_dma(st, p)
-    st.branch("s_branch", L["end"][p])
-    st.label(idle)
-    next_dma(st)
-    st.branch("s_branch", L["end"][p])
-    st.label(nodma)
     st.raw(f"s_cmp_lt_u32 {SJ}, {SNW}")
     st.branch("s_cbranch_scc0", L["end"][p])
     for b in range(4):
@@ -832,66 +810,6 @@ def pstamp(st, dst):
         st.raw(f"s_memtime s[{dst}:{dst + 1}]")
         st.raw("s_waitcnt lgkmcnt(0)")
         st.lgkm = []
-
-
-def next_dma_groups():
-    """the next item's LDS-DMA pieces (see next_dma) as instruction groups,
-    to be placed between MFMAs; s39 keeps m0, ST0 = qwn * 256 (set first)"""
-    groups = []
-    for i in range(16):
-        b, t = divmod(i, 4)
-        groups.append([f"s_add_u32 {ST1}, {ST0}, {4096 * b + 64 * t}",
-                       f"s_add_u32 m0, %[qlw], {1024 * i}", "s_nop 0",
-                       f"buffer_load_dwordx4 %[qoff], %[rqn], {ST1} offen lds"])
-    for kt in range(2):
-        for i in range(4):
-            groups.append([f"s_mov_b32 {ST1}, {16384 * kt + 4096 * i}",
-                           f"s_add_u32 m0, %[kdw], {KBUF[kt] + 4096 * i}", "s_nop 0",
-                           f"buffer_load_dwordx4 %[kdma], %[rkn], {ST1} offen lds"])
-    return groups
-
-
-def pv_dma(st, p):
-    """pv_plain with the next item's DMA pieces in every third MFMA gap"""
-    vb = VBUF[p]
-    mf, frag_first = pv_mfmas()
-    gaps = {}
-    for f in range(16):
-        u, e = divmod(f, 8)
-        k = frag_first[f - 2] + 1 if f >= 2 else 0
-        for i, r in enumerate(v_reads(u, e, f % 8, vb)):
-            gaps.setdefault(k + i if f >= 2 else 0, []).append(r)
-    st.raw("s_mov_b32 s39, m0")
-    st.raw(f"s_lshl_b32 {ST0}, %[qwn], 8")
-    for g, grp in enumerate(next_dma_groups()):
-        gaps.setdefault(2 + 3 * g, []).extend(grp)
-    st.interleave(mf, gaps)
-    st.raw("s_mov_b32 m0, s39")
-
-
-def next_dma(st):
-    """LDS-DMA (buffer_load ... lds) of the NEXT item's operands, issued in
-    this item's last iteration once both K images are dead: this wave's 64 Q
-    rows into its QBUF region (lane-linear: piece 4b+t holds what the cold
-    prologue's load (b, t) puts in v[16b+4t]) and its quarter of K(0), K(1)
-    into KBUF 0/1 (the source chunk per lane chosen so the lane-linear write
-    lands in the k_off16 image).  The next item's prologue then loads only
-    V(0) and stage 0 from memory."""
-    st.raw("s_mov_b32 s39, m0")
-    st.raw(f"s_lshl_b32 {ST0}, %[qwn], 8")
-    for i in range(16):
-        b, t = divmod(i, 4)
-        st.raw(f"s_add_u32 {ST1}, {ST0}, {4096 * b + 64 * t}")
-        st.raw(f"s_add_u32 m0, %[qlw], {1024 * i}")
-        st.raw("s_nop 0")
-        st.raw(f"buffer_load_dwordx4 %[qoff], %[rqn], {ST1} offen lds")
-    for kt in range(2):
-        for i in range(4):
-            st.raw(f"s_mov_b32 {ST1}, {16384 * kt + 4096 * i}")
-            st.raw(f"s_add_u32 m0, %[kdw], {KBUF[kt] + 4096 * i}")
-            st.raw("s_nop 0")
-            st.raw(f"buffer_load_dwordx4 %[kdma], %[rkn], {ST1} offen lds")
-    st.raw("s_mov_b32 m0, s39")
 
 
 def stage0(st):
@@ -945,9 +863,13 @@ def q_scale(st):
 
 def prologue(st, causal):
     """Q (scaled), K(0), K(1), V(0) into registers / LDS, stage 0 in flight,
-    S(0) = K(0) Q^T with the first-tile rescale and exp2.  Cold (the
-    workgroup's first item): everything from memory.  Warm (%[flags] bit 1):
-    Q, K(0), K(1) arrived by LDS-DMA during the previous item (next_dma)."""
+    S(0) = K(0) Q^T with the first-tile rescale and exp2.  V(0) and K(1)
+    are waited for only after S(0) (their latency under the Q scaling, the
+    QK^T and the first softmax).  (Prefetching the next item's Q, K(0), K(1)
+    by LDS-DMA during the previous item's last iteration cut this prologue
+    from 11.4k to 6.2k cycles at the headline but added as much to the
+    loop -- the DMA issue cost -- and was dropped:
+    profiles/r03_ab_w4_next_item_dma.jsonl.)"""
     pstamp(st, 60)
     st.raw("s_mov_b32 s40, %[rk0]")
     st.raw("s_mov_b32 s41, %[rk1]")
@@ -969,10 +891,6 @@ def prologue(st, causal):
     for i in range(1, 4):
         st.raw(f"v_add_u32 {KOFF[i]}, {4096 * i}, %[koff]")
         st.raw(f"v_add_u32 {VOFF[i]}, {4096 * i}, %[voff]")
-    warm, join = newlabel("warm"), newlabel("join")
-    st.raw("s_bitcmp1_b32 %[flags], 1")
-    st.branch("s_cbranch_scc1", warm)
-    # ---- cold ----
     # Q rows qw + 16b + r16: offset (qw + 16b) * 256 + %[qoff]
     st.raw(f"s_lshl_b32 {ST0}, %[qw], 8")
     for b in range(4):
@@ -1003,23 +921,6 @@ def prologue(st, causal):
     q_scale(st)
     st.raw("s_waitcnt lgkmcnt(0)")
     st.raw("s_barrier")
-    st.branch("s_branch", join)
-    # ---- warm ----
-    st.label(warm)
-    # the DMA pieces (older than the previous item's 16 O stores) landed,
-    # in every wave
-    st.raw("s_waitcnt vmcnt(16)")
-    st.raw("s_barrier")
-    for i in range(16):
-        b, t = divmod(i, 4)
-        st.raw(f"ds_read_b128 {R('v', 16 * b + 4 * t, 4)}, %[qrd] offset:{1024 * i}")
-    for i in range(4):
-        st.raw(f"buffer_load_dwordx4 {vst(i, 1)}, {VOFF[i]}, {SV}, 0 offen")
-    stage0(st)
-    zero_state(st)
-    st.raw("s_waitcnt lgkmcnt(0)")
-    q_scale(st)
-    st.label(join)
     st.nop(2)
     # S(0)
     qk_plain(st, KBUF[0])
@@ -1033,16 +934,11 @@ def prologue(st, causal):
     slow_softmax(st, first=True)
     for e in exp_ops():
         st.emit(e)
-    # V(0) (and on the cold path K(1)) landed: into their LDS images
+    # V(0), K(1) landed: into their LDS images
     st.raw("s_waitcnt vmcnt(8)")
     for i in range(4):
         st.raw(f"ds_write_b128 %[vlds], {vst(i, 1)} offset:{VBUF[0] + 4096 * i}")
-    nok1 = newlabel("nok1")
-    st.raw("s_bitcmp1_b32 %[flags], 1")
-    st.branch("s_cbranch_scc1", nok1)
-    for i in range(4):
         st.raw(f"ds_write_b128 %[klds], {kst(i, 1)} offset:{KBUF[1] + 4096 * i}")
-    st.label(nok1)
     st.raw("s_waitcnt lgkmcnt(0)")
     st.lgkm = []
     st.raw("s_barrier")
@@ -1166,7 +1062,7 @@ def cxx(causal, bf16, lines, split=False):
     body = "\n".join(f'      "{l}\\n"' for l in lines)
     vclob = ", ".join(f'"v{i}"' for i in range(236))
     aclob = ", ".join(f'"a{i}"' for i in range(240 if STAGE2 else 208))
-    sclob = ", ".join(f'"s{i}"' for i in range(39, 70 if DIAG in ("stamps", "pstamps") else 60))
+    sclob = ", ".join(f'"s{i}"' for i in range(40, 70 if DIAG in ("stamps", "pstamps") else 60))
     name = (("w4_item_causal" if causal else "w4_item_noncausal") + ("_split" if split else "")
             + ("_bf16" if bf16 else "_f16"))
     return f"""
@@ -1177,14 +1073,12 @@ __device__ __forceinline__ void {name}(const W4Item& it, const W4Lane& ln) {{
       : [rq] "s"(it.rq), [ro] "s"(it.ro),
         [rk0] "s"(it.rk0), [rk1] "s"(it.rk1), [rk2] "s"(it.rk2), [rk3] "s"(it.rk3),
         [rv0] "s"(it.rv0), [rv1] "s"(it.rv1), [rv2] "s"(it.rv2), [rv3] "s"(it.rv3),
-        [qw] "s"(it.qw), [qm] "s"(it.qm), [rl] "s"(it.rl),
-        [rqn] "s"(it.rqn), [rkn] "s"(it.rkn), [qwn] "s"(it.qwn), [flags] "s"(it.flags),
-        [qlw] "s"(it.qlw), [kdw] "s"(it.kdw), [ntiles] "s"(it.ntiles), [nw] "s"(it.nw), [masklast] "s"(it.masklast),
+        [qw] "s"(it.qw), [qm] "s"(it.qm), [rl] "s"(it.rl), [ntiles] "s"(it.ntiles), [nw] "s"(it.nw), [masklast] "s"(it.masklast),
         [kvhi] "s"(it.kvhi), [c] "s"(it.c),
         [ka0] "v"(ln.ka[0]), [ka1] "v"(ln.ka[1]), [ka2] "v"(ln.ka[2]), [ka3] "v"(ln.ka[3]),
         [va0] "v"(ln.va[0]), [va1] "v"(ln.va[1]), [koff] "v"(ln.koff), [voff] "v"(ln.voff),
         [klds] "v"(ln.klds), [vlds] "v"(ln.vlds), [vt] "v"(ln.vt), [r16] "v"(ln.r16),
-        [qoff] "v"(ln.qoff), [ooff] "v"(ln.ooff), [qrd] "v"(ln.qrd), [kdma] "v"(ln.kdma)
+        [qoff] "v"(ln.qoff), [ooff] "v"(ln.ooff)
       : "memory", "vcc", "scc", {sclob},
         {vclob},
         {aclob});

@@ -138,11 +138,11 @@ def load_library() -> ctypes.CDLL:
     lib.fa_splitkv_o_bytes.restype = ull
     lib.fa_splitkv_ml_bytes.argtypes = [i, i, i, i, i]
     lib.fa_splitkv_ml_bytes.restype = ull
-    lib.fa_fwd_f16_ws.argtypes = [vp, vp, vp, vp, i, i, i, i, i, vp, ull, vp]
+    lib.fa_fwd_f16_ws.argtypes = [vp, vp, vp, vp, i, i, i, i, i, i, vp, ull, vp]
     lib.fa_fwd_f16_ws.restype = i
-    lib.fa_fwd_bf16_ws.argtypes = [vp, vp, vp, vp, i, i, i, i, i, vp, ull, vp]
+    lib.fa_fwd_bf16_ws.argtypes = [vp, vp, vp, vp, i, i, i, i, i, i, vp, ull, vp]
     lib.fa_fwd_bf16_ws.restype = i
-    lib.fa_fwd_ws_bytes.argtypes = [i, i, i, i, i]
+    lib.fa_fwd_ws_bytes.argtypes = [i, i, i, i, i, i]
     lib.fa_fwd_ws_bytes.restype = ull
     lib.fa_fwd_split_pieces.argtypes = [i, i, i, i, i]
     lib.fa_fwd_split_pieces.restype = i
@@ -249,21 +249,23 @@ def _check_qkvo_each(q, k, v, out):
                                       f"{name} is on {t.device}, q on {q.device}: one device only")
 
 
-_WS_NEED = {}  # (device, B, H, S, D, causal) -> workspace bytes (fa_fwd_ws_bytes)
+_WS_NEED = {}  # (device, B, H, S, D, causal, piece_tiles) -> workspace bytes (fa_fwd_ws_bytes)
 _WS_BUF = {}   # (device, stream) -> zero-filled uint8 workspace, kept for the process
 
 
 def workspace_bytes(batch: int, heads: int, seq_len: int, head_dim: int, causal: bool,
-                    device=None) -> int:
-    """Workspace the split tier needs for this shape on `device` (0: no split)."""
+                    device=None, piece_tiles: int = 0) -> int:
+    """Workspace the split tier needs for this call on `device` (0: no split);
+    piece_tiles as in :func:`flash_attention_fwd`."""
     import torch
 
     dev = torch.cuda.current_device() if device is None else torch.device(device).index
-    key = (dev, batch, heads, seq_len, head_dim, bool(causal))
+    key = (dev, batch, heads, seq_len, head_dim, bool(causal), int(piece_tiles))
     n = _WS_NEED.get(key)
     if n is None:
         with torch.cuda.device(dev):
-            n = load_library().fa_fwd_ws_bytes(batch, heads, seq_len, head_dim, int(bool(causal)))
+            n = load_library().fa_fwd_ws_bytes(batch, heads, seq_len, head_dim, int(bool(causal)),
+                                               int(piece_tiles))
         _WS_NEED[key] = n
     return n
 
@@ -279,6 +281,8 @@ def _workspace(nbytes: int, dev: int, st: int):
         return torch.zeros(nbytes, dtype=torch.uint8, device=dev)
     buf = _WS_BUF.get((dev, st))
     if buf is None or buf.numel() < nbytes:
+        if buf is not None:
+            torch.cuda.synchronize(dev)  # launches enqueued on the old one are done
         buf = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
         torch.cuda.current_stream(dev).synchronize()  # the fill lands before any stream uses it
         _WS_BUF[(dev, st)] = buf
@@ -286,16 +290,18 @@ def _workspace(nbytes: int, dev: int, st: int):
 
 
 def flash_attention_fwd(q, k, v, causal: bool = False, out=None, config: Optional[int] = None,
-                        stream=None):
+                        stream=None, piece_tiles: int = 0):
     """O = softmax(Q K^T / sqrt(D) [+ causal mask]) V for fp16 or bf16 BHSD tensors.
 
     q, k, v: [batch, heads, seq_len, D] float16 (the reference's type) or
     bfloat16 contiguous device tensors, all of one dtype; D = 128 (the
     reference's head_dim) or 64.
     config: force a tile config id (see :func:`configs`); default = dispatcher,
-    which for short causal shapes splits query blocks' key ranges across
-    workgroups through a workspace from torch's caching allocator
-    (fa_fwd_*_ws; :func:`workspace_bytes`).
+    which for long causal launches short of the persistent tier splits query
+    blocks' key ranges across workgroups through a workspace from torch's
+    caching allocator (fa_fwd_*_ws; :func:`workspace_bytes`).
+    piece_tiles > 0 (causal, head_dim 128, config None): force that split
+    piece length in 64-key tiles.
     Enqueued on ``stream`` (default: torch's current stream); no sync.
     """
     import torch
@@ -313,12 +319,12 @@ def flash_attention_fwd(q, k, v, causal: bool = False, out=None, config: Optiona
         st = stream if isinstance(stream, int) else stream.cuda_stream
     args = (q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), b, h, s, d, int(bool(causal)))
     if config is None:
-        need = _WS_NEED.get((dev, b, h, s, d, bool(causal)))
+        need = _WS_NEED.get((dev, b, h, s, d, bool(causal), piece_tiles))
         if need is None:
-            need = workspace_bytes(b, h, s, d, causal, device=q.device)
-        if need:
+            need = workspace_bytes(b, h, s, d, causal, device=q.device, piece_tiles=piece_tiles)
+        if need or piece_tiles:
             fn = lib.fa_fwd_bf16_ws if bf16 else lib.fa_fwd_f16_ws
-            args += (_workspace(need, dev, st).data_ptr(), need)
+            args += (int(piece_tiles), _workspace(need, dev, st).data_ptr() if need else None, need)
         else:
             fn = lib.fa_fwd_bf16 if bf16 else lib.fa_fwd_f16
     else:

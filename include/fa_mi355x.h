@@ -116,27 +116,34 @@ unsigned long long fa_splitkv_ml_bytes(int batch, int heads, int seq_len,
                                        int head_dim, int num_splits);
 
 /* Workspace forward: fa_fwd_f16 / fa_fwd_bf16 plus a caller-owned device
- * workspace that lets short causal launches split each query block's key
- * range across workgroups and merge the pieces in the same launch (the
- * reference's split-K LSE merge, :559-598, without a second kernel).
- * fa_fwd_ws_bytes() is the workspace this shape needs on the current device,
- * 0 when the dispatcher does not split it (the _ws entries then run exactly
- * fa_fwd_f16 / fa_fwd_bf16 and ignore the workspace).  The workspace must be
- * zero-filled before its first use; every launch leaves it reusable (its
- * arrival counters back at zero), so one buffer serves any number of
- * launches on ONE stream (launches on different streams need their own).
- * FA_ERR_WORKSPACE if the shape splits and workspace is NULL or ws_bytes is
- * short.  fa_fwd_split_pieces() is the key-piece length in 64-key tiles the
- * dispatcher would use (0 = no split). */
+ * workspace that lets causal launches short of the persistent tier split each
+ * 256-row query block's key range into pieces run by separate workgroups and
+ * merge them in the same launch (the reference's split-K log-sum-exp merge,
+ * :559-598, without its second kernel; fp16 / bf16 normalised partial rows
+ * plus an fp32 log2-sum-exp per row).
+ *   piece_tiles = 0: the dispatcher's choice -- fa_fwd_split_pieces() is its
+ *     piece length in 64-key tiles, 0 when it does not split this shape (the
+ *     _ws entries then run exactly fa_fwd_f16 / fa_fwd_bf16 and ignore the
+ *     workspace);
+ *   piece_tiles > 0: that piece length (causal, head_dim 128, at most 8
+ *     pieces per query block, else FA_ERR_BAD_CONFIG).
+ * fa_fwd_ws_bytes() is the workspace the call needs (0: no split).  Its
+ * first 64 KB (arrival counters, the same place for every shape) must be
+ * zero before the first use; every launch returns the counters it used to
+ * zero, so one buffer of the largest size needed serves any sequence of
+ * shapes on ONE stream (launches on different streams need their own).  FA_ERR_WORKSPACE if the call splits and workspace is NULL or
+ * ws_bytes is short. */
 unsigned long long fa_fwd_ws_bytes(int batch, int heads, int seq_len, int head_dim,
-                                   int causal);
+                                   int causal, int piece_tiles);
 int fa_fwd_split_pieces(int batch, int heads, int seq_len, int head_dim, int causal);
 int fa_fwd_f16_ws(const void* q, const void* k, const void* v, void* o,
                   int batch, int heads, int seq_len, int head_dim, int causal,
-                  void* workspace, unsigned long long ws_bytes, void* hip_stream);
+                  int piece_tiles, void* workspace, unsigned long long ws_bytes,
+                  void* hip_stream);
 int fa_fwd_bf16_ws(const void* q, const void* k, const void* v, void* o,
                    int batch, int heads, int seq_len, int head_dim, int causal,
-                   void* workspace, unsigned long long ws_bytes, void* hip_stream);
+                   int piece_tiles, void* workspace, unsigned long long ws_bytes,
+                   void* hip_stream);
 
 /* The dispatcher's decision (ref tier table :620-661): config id used by
  * fa_fwd_f16 for this shape. */

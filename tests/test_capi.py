@@ -89,8 +89,6 @@ def test_config_table():
         need = 2 * nbuf * c.block_n * 256
         if "_pingpong_persistent_" in c.name and "_dma_" not in c.name and not c.causal:
             need = max(need, KVPAIR_LDS)  # room for the KV-pair tail halves
-        if "_w4x64_" in c.name:
-            need += 256 * 256  # the next item's Q rows (LDS-DMA prefetch)
         assert c.lds_bytes == need <= 160 * 1024
     # every (waves, bn) non-split config exists for both masks
     nonsplit = {(c.waves, c.block_n, c.causal) for c in cfgs if not c.split_kv}
@@ -297,19 +295,28 @@ def test_split_plan_and_workspace_entry():
     and the workspace entry's argument checks -- no launch, no GPU needed."""
     fa = _fa()
     lib = fa.load_library()
-    # short causal: pieces of >= 4 tiles; B=1 H=32 S=1024 -> 8 pieces of 6 per head
-    t = lib.fa_fwd_split_pieces(1, 32, 1024, 128, 1)
-    assert t >= 4
-    need = lib.fa_fwd_ws_bytes(1, 32, 1024, 128, 1)
-    assert need > 0 and need % 256 == 0
-    # no split: non-causal, head_dim 64, the persistent tier's shapes, S < 512
-    for args in ((1, 32, 1024, 128, 0), (1, 32, 1024, 64, 1), (64, 32, 4096, 128, 1),
-                 (1, 32, 8192, 128, 1), (1, 32, 256, 128, 1)):
+    # the dispatcher splits long causal launches short of the persistent tier
+    for b, h, s in ((1, 4, 4096), (1, 8, 4096), (1, 4, 8192), (1, 2, 16384), (1, 1, 32768)):
+        t = lib.fa_fwd_split_pieces(b, h, s, 128, 1)
+        assert t >= 4, (b, h, s)
+        need = lib.fa_fwd_ws_bytes(b, h, s, 128, 1, 0)
+        assert need > 0 and need % 256 == 0
+    # no split: non-causal, head_dim 64, the persistent tier's shapes, S < 4096
+    for args in ((1, 4, 4096, 128, 0), (1, 4, 4096, 64, 1), (64, 32, 4096, 128, 1),
+                 (1, 32, 8192, 128, 1), (1, 32, 1024, 128, 1), (1, 8, 2048, 128, 1)):
         assert lib.fa_fwd_split_pieces(*args) == 0, args
-        assert lib.fa_fwd_ws_bytes(*args) == 0, args
+        assert lib.fa_fwd_ws_bytes(*args, 0) == 0, args
+    # a forced piece length: sizes grow with the pieces per block; > 8 pieces,
+    # non-causal or one piece per block is not a split
+    assert lib.fa_fwd_ws_bytes(1, 32, 1024, 128, 1, 6) > 0
+    assert lib.fa_fwd_ws_bytes(1, 32, 1024, 128, 1, 1) == 0   # 16 pieces
+    assert lib.fa_fwd_ws_bytes(1, 32, 1024, 128, 0, 6) == 0
+    assert lib.fa_fwd_ws_bytes(1, 32, 1024, 128, 1, 16) == 0  # one piece
+    need = lib.fa_fwd_ws_bytes(1, 4, 4096, 128, 1, 0)
     p = ctypes.c_void_p(0x1000)
-    assert lib.fa_fwd_f16_ws(p, p, p, p, 1, 32, 1024, 128, 1, None, need, None) == fa.FA_ERR_WORKSPACE
-    assert lib.fa_fwd_f16_ws(p, p, p, p, 1, 32, 1024, 128, 1, p, need - 1, None) == fa.FA_ERR_WORKSPACE
-    assert lib.fa_fwd_bf16_ws(p, p, p, p, 1, 32, 1024, 96, 1, p, need, None) == \
+    assert lib.fa_fwd_f16_ws(p, p, p, p, 1, 4, 4096, 128, 1, 0, None, need, None) == fa.FA_ERR_WORKSPACE
+    assert lib.fa_fwd_f16_ws(p, p, p, p, 1, 4, 4096, 128, 1, 0, p, need - 1, None) == fa.FA_ERR_WORKSPACE
+    assert lib.fa_fwd_f16_ws(p, p, p, p, 1, 32, 1024, 128, 1, 1, p, 1 << 30, None) == fa.FA_ERR_BAD_CONFIG
+    assert lib.fa_fwd_bf16_ws(p, p, p, p, 1, 4, 4096, 96, 1, 0, p, need, None) == \
         fa.FA_ERR_UNSUPPORTED_HEAD_DIM
-    assert lib.fa_fwd_f16_ws(None, p, p, p, 1, 32, 1024, 128, 1, p, need, None) == fa.FA_ERR_NULL_POINTER
+    assert lib.fa_fwd_f16_ws(None, p, p, p, 1, 4, 4096, 128, 1, 0, p, need, None) == fa.FA_ERR_NULL_POINTER
