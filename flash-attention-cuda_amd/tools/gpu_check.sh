@@ -7,7 +7,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out
-R=${ROUND:-r03}
+R=${ROUND:-r02}
 mkdir -p $OUT
 step() { echo "[$(date +%T)] $*" >&2; }
 
