@@ -33,7 +33,7 @@ import json
 import os
 import sys
 
-SHAPES = [  # (label, batch, heads, seq, causal)
+SHAPES = [  # (label, batch, heads, seq, causal[, forced tier name | "auto"])
     ("cfg0_s512_noncausal", 1, 32, 512, False),
     ("cfg1_s1024_causal", 1, 32, 1024, True),
     ("s1024_noncausal", 1, 32, 1024, False),
@@ -45,8 +45,18 @@ SHAPES = [  # (label, batch, heads, seq, causal)
     ("cfg4_b8_s4096_causal_shard", 8, 32, 4096, True),   # one GPU's shard of config 5 at N=8
     ("headline_b64_s4096_causal", 64, 32, 4096, True),
     ("s256_b16_noncausal", 16, 32, 256, False),
+    # the causal split tier (workspace entry; the default Python path)
+    ("split_h8_s4096_causal", 1, 8, 4096, True, "auto"),
+    ("split_h4_s8192_causal", 1, 4, 8192, True, "auto"),
     # non-dispatched tile configs (BM, BN, waves) on the same shapes: the
-    # per-item 8-wave ping-pong (what the persistent order buys)
+    # 8-wave persistent ping-pong W4 replaced, BN=128 (the reference's long
+    # non-causal tile), the per-item ping-pong (what the persistent order buys)
+    ("pingpong_s8192_noncausal", 1, 32, 8192, False, "bm256_bn64_w8_m16_pingpong_persistent_noncausal"),
+    ("pingpong_s8192_causal", 1, 32, 8192, True, "bm256_bn64_w8_m16_pingpong_persistent_causal"),
+    ("pingpong_headline_b64_s4096_causal", 64, 32, 4096, True,
+     "bm256_bn64_w8_m16_pingpong_persistent_causal"),
+    ("bn128_s8192_noncausal", 1, 32, 8192, False, "bm128_bn128_w4_m16_noncausal"),
+    ("bn128_s8192_causal", 1, 32, 8192, True, "bm128_bn128_w4_m16_causal"),
     ("pingpong_item_s8192_causal", 1, 32, 8192, True, "bm256_bn64_w8_m16_pingpong_causal"),
 ]
 ITERS = 6
@@ -69,7 +79,7 @@ def run(time_it):
         q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5, generator=g)
                    for _ in range(3))
         o = torch.empty_like(q)
-        cfg = names[forced[0]] if forced else fa.select_config(b, h, s, causal)
+        cfg = (None if forced[0] == "auto" else names[forced[0]]) if forced else fa.select_config(b, h, s, causal)
         fwd = lambda: fa.flash_attention_fwd(q, k, v, causal, out=o, config=cfg)
         flops = fa.attention_flops(b, h, s, 128, causal)
         torch.cuda.synchronize()
@@ -88,7 +98,9 @@ def run(time_it):
                 best.append(st.elapsed_time(en) / n)
             ms = sorted(best)[1]
             print(json.dumps({"label": label, "batch": b, "heads": h, "seq": s, "causal": causal,
-                              "config": fa.configs()[cfg].name, "ms": ms,
+                              "config": (fa.configs()[cfg].name if cfg is not None else
+                                         "split_T%d" % fa.load_library().fa_fwd_split_pieces(b, h, s, 128, int(causal))),
+                              "ms": ms,
                               "tflops": flops / (ms / 1e3) / 1e12, "flops": flops,
                               "alg_bytes": 8.0 * b * h * s * 128}), flush=True)
         else:
