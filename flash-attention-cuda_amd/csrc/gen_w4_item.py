@@ -77,7 +77,7 @@ def set_dtype(bf16):
               if bf16 else {"mfma": "v_mfma_f32_16x16x32_f16", "cvt_pk": "v_cvt_pk_f16_f32",
                             "one2": "0x3c003c00"})
     DT["bf16"] = bf16
-V_AHEAD = 3           # V^T fragments read ahead of the PV MFMAs that use them
+V_AHEAD = int(os.environ.get("W4_V_AHEAD", "3"))  # V^T fragments read ahead of the PV MFMAs that use them
 
 
 def regs(spec):
@@ -443,6 +443,8 @@ def stage_loads(st_set=0):
     for i in range(4):
         out.append(vmem(f"buffer_load_dwordx4 {kst(i, st_set)}, {KOFF[i]}, {SK}, 0 offen", r=[KOFF[i]], w=[kst(i, st_set)]))
         out.append(vmem(f"buffer_load_dwordx4 {vst(i, st_set)}, {VOFF[i]}, {SV}, 0 offen", r=[VOFF[i]], w=[vst(i, st_set)]))
+    if "noadv" in XP:  # timing only: every stage re-reads the same (L1-hot) tile
+        return out + [salu("s_nop 0")] * 8
     out += [salu("s_add_u32 s40, s40, 0x4000"), salu("s_addc_u32 s41, s41, 0"),
             salu(f"s_sub_i32 {SKREM}, {SKREM}, 0x4000"), salu(f"s_max_i32 s42, {SKREM}, 0"),
             salu("s_add_u32 s44, s44, 0x4000"), salu("s_addc_u32 s45, s45, 0"),
@@ -520,7 +522,7 @@ def phase_a(st, p, with_max):
     # the first V^T fragments of PV(j) (V(j) is ready since the last barrier)
     for f in range(V_AHEAD):
         for i, r in enumerate(v_reads(0, f, f, VBUF[p])):
-            put(52 + 3 * f + i, r)
+            put(52 - 3 * (V_AHEAD - 3) + 3 * f + i, r)
     st.interleave(mf, gaps)
     leftover = []
     if with_max and "nomax" not in XP:
