@@ -101,7 +101,8 @@ __global__ __launch_bounds__(WAVES * 64, BN == 128 ? 1 : 2) void fa_fwd_f16_kern
     g_fa_timeline[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
     g_fa_timeline[blockIdx.x][3] = __builtin_amdgcn_s_memtime() - c_start;
     g_fa_timeline[blockIdx.x][2] =
-        (unsigned long long)hw | ((unsigned long long)xcc << 32) | ((unsigned long long)qb << 40);
+        (unsigned long long)hw | ((unsigned long long)xcc << 32) | ((unsigned long long)(qb & 0xFFFF) << 40) |
+        ((unsigned long long)(bh & 0xFF) << 56);
   }
 #endif
 }
@@ -235,7 +236,8 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(
         g_fa_timeline[rec][1] = __builtin_amdgcn_s_memrealtime();
         g_fa_timeline[rec][3] = __builtin_amdgcn_s_memtime() - c_start;
         g_fa_timeline[rec][2] =
-            (unsigned long long)hw | ((unsigned long long)xcc << 32) | ((unsigned long long)qb << 40);
+            (unsigned long long)hw | ((unsigned long long)xcc << 32) | ((unsigned long long)(qb & 0xFFFF) << 40) |
+        ((unsigned long long)(bh & 0xFF) << 56);
       }
 #endif
     }
@@ -282,7 +284,8 @@ __global__ __launch_bounds__(512, 2) void fa_fwd_f16_kvpair_kernel(FwdParams p) 
     g_fa_timeline[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
     g_fa_timeline[blockIdx.x][3] = __builtin_amdgcn_s_memtime() - c_start;
     g_fa_timeline[blockIdx.x][2] =
-        (unsigned long long)hw | ((unsigned long long)xcc << 32) | ((unsigned long long)qb << 40);
+        (unsigned long long)hw | ((unsigned long long)xcc << 32) | ((unsigned long long)(qb & 0xFFFF) << 40) |
+        ((unsigned long long)(bh & 0xFF) << 56);
   }
 #endif
 }
@@ -940,11 +943,18 @@ extern "C" int fa_debug_timeline(unsigned long long* out, int n) {
              : FA_ERR_HIP;
 }
 extern "C" int fa_debug_stamps(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fa::g_fa_stamps), sizeof(fa::g_fa_stamps)) != hipSuccess)
+  static unsigned long long all[64][8][12];  // the first 64 workgroups' slots, summed below
+  static_assert(sizeof(all) == sizeof(fa::g_fa_stamps), "one slot per workgroup");
+  if (hipMemcpyFromSymbol(all, HIP_SYMBOL(fa::g_fa_stamps), sizeof(all)) != hipSuccess)
     return FA_ERR_HIP;
+  for (int w = 0; w < 8; ++w)
+    for (int i = 0; i < 12; ++i) {
+      unsigned long long t = 0;
+      for (int b = 0; b < 64; ++b) t += all[b][w][i];
+      out[w * 12 + i] = t;
+    }
   if (reset) {
-    static const unsigned long long z[8][12] = {};
-    static_assert(sizeof(z) == sizeof(fa::g_fa_stamps), "reset covers every stamp");
+    static const unsigned long long z[64][8][12] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(fa::g_fa_stamps), z, sizeof(z)) != hipSuccess) return FA_ERR_HIP;
   }
   return FA_OK;

@@ -206,9 +206,11 @@ __device__ __forceinline__ int lds_addr(const void* p) {
 
 #ifdef FA_STAMPS
 // diagnostic build only (lib/libfa_mi355x_stamps.so): per-wave cycles spent in
-// [MFMA block, barrier after it, softmax block, barrier after it, LDS tile write], summed over
-// the first 64 workgroups.  Never part of the product library.
-__device__ unsigned long long g_fa_stamps[8][12];  // 5 phases, issue_tile, iterations, prologue, epilogue, items
+// [MFMA block, barrier after it, softmax block, barrier after it, LDS tile write] of
+// the first 64 workgroups, one slot each (plain stores: atomics on shared
+// counters would slow exactly those workgroups and show in the timeline),
+// summed by fa_debug_stamps.  Never part of the product library.
+__device__ unsigned long long g_fa_stamps[64][8][12];  // 5 phases, issue_tile, iterations, prologue, epilogue, items
 // per-workgroup timeline: {start, end (s_memrealtime, 100 MHz), hw_id | xcc_id << 32 | qb << 40,
 //                          shader cycles (s_memtime) start..end}
 constexpr int FA_MAX_TIMELINE = 65536;
@@ -850,7 +852,7 @@ __device__ __forceinline__ void attention_tile_loop(const FwdParams& p, int bh, 
   if (j < ntiles) step(j, std::integral_constant<int, 0>{});
 #ifdef FA_STAMPS
   if (lane == 0 && blockIdx.x < 64)
-    for (int i = 0; i < 12; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
+    for (int i = 0; i < 12; ++i) g_fa_stamps[blockIdx.x][wave][i] += st_acc[i];  // this wave's own slot
 #endif
 #undef FA_TSTAMP
 
@@ -1135,7 +1137,7 @@ __device__ __forceinline__ void attention_pingpong(const FwdParams& p, int bh, i
   __builtin_amdgcn_s_waitcnt(0);  // stores issued and retired
   st_acc[8] = __builtin_amdgcn_s_memtime() - t_le;
   if (lane == 0 && blockIdx.x < 64)
-    for (int i = 0; i < 11; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
+    for (int i = 0; i < 11; ++i) g_fa_stamps[blockIdx.x][wave][i] += st_acc[i];  // this wave's own slot
 #endif
 #undef FA_STAMP
 }
@@ -1429,7 +1431,7 @@ __device__ __forceinline__ void attention_kvpair(const FwdParams& p, int bh, int
   st_acc[8] = __builtin_amdgcn_s_memtime() - t_le;  // merge + stores retired
   st_acc[9] = 1;
   if (lane == 0 && blockIdx.x < 64)
-    for (int i = 0; i < 12; ++i) atomicAdd(&g_fa_stamps[wave][i], st_acc[i]);
+    for (int i = 0; i < 12; ++i) g_fa_stamps[blockIdx.x][wave][i] += st_acc[i];  // this wave's own slot
 #endif
 #undef FA_KSTAMP
 }

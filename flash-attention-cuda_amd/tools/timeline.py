@@ -57,10 +57,12 @@ print(f"  last 1% of workgroups end after {ends[int(0.99*len(ends))]:.1f} us; "
 # per-CU gaps between consecutive workgroups, and duration vs query block
 percu = collections.defaultdict(list)
 byqb = collections.defaultdict(list)
+byh = collections.defaultdict(list)
 for s_, e_, hw in rows:
     h = hw & 0xFFFFFFFF
     percu[((hw >> 32) & 0xFF, (h >> 13) & 7, (h >> 12) & 1, (h >> 8) & 15)].append((s_, e_))
     byqb[(hw >> 40) & 0xFFFF].append((e_ - s_) / 100.0)
+    byh[(hw >> 56) & 0xFF].append((e_ - s_) / 100.0)
 gaps = []
 for lst in percu.values():
     lst.sort()
@@ -78,3 +80,30 @@ if len(pts) > 2:
     sl = sum((p_[0] - mx) * (p_[1] - my) for p_ in pts) / sum((p_[0] - mx) ** 2 for p_ in pts)
     print(f"  duration ~ {my - sl * mx:.2f} us + {sl:.3f} us x (qb+1)   [causal: per 256-row key step]")
     print("  qb:dur " + " ".join(f"{x}:{sum(byqb[x])/len(byqb[x]):.1f}" for x in xs[:32]))
+    bys = collections.defaultdict(list)
+    for s_, e_, hw in rows:
+        bys[(hw >> 40) & 0xFFFF].append((s_ - t0) / 100.0)
+    print("  qb:start " + " ".join(f"{x}:{sum(bys[x])/len(bys[x]):.1f}/{max(bys[x]):.1f}" for x in xs[:32]))
+    # per-XCD busy: are the heavy blocks on a few XCDs / sharing CUs?
+    percu_n = collections.Counter(((hw >> 32) & 0xFF, ((hw & 0xFFFFFFFF) >> 13) & 7, ((hw & 0xFFFFFFFF) >> 12) & 1, ((hw & 0xFFFFFFFF) >> 8) & 15) for _, _, hw in rows)
+    print("  WGs per CU histogram:", dict(collections.Counter(percu_n.values())))
+    # shader engine / array of each query block's workgroups, and duration by SE
+    se_qb = collections.defaultdict(collections.Counter)
+    dur_se = collections.defaultdict(list)
+    for s_, e_, hw in rows:
+        h = hw & 0xFFFFFFFF
+        se, sa = (h >> 13) & 7, (h >> 12) & 1
+        se_qb[(hw >> 40) & 0xFFFF][(se, sa)] += 1
+        dur_se[(se, sa)].append((e_ - s_) / 100.0)
+    print("  qb -> (se,sa):count " + " | ".join(
+        f"{x}:" + ",".join(f"{k[0]}{k[1]}:{v}" for k, v in sorted(se_qb[x].items())) for x in xs[:16]))
+    dur_x = collections.defaultdict(list)
+    dur_cu = collections.defaultdict(list)
+    for s_, e_, hw in rows:
+        h = hw & 0xFFFFFFFF
+        dur_x[(hw >> 32) & 0xFF].append((e_ - s_) / 100.0)
+        dur_cu[(h >> 8) & 15].append((e_ - s_) / 100.0)
+    print("  dur by head: " + " ".join(f"{k}:{sum(v)/len(v):.0f}/{max(v):.0f}" for k, v in sorted(byh.items())[:64]))
+    print("  dur by xcc: " + " ".join(f"{k}:{sum(v)/len(v):.1f}/{max(v):.1f}" for k, v in sorted(dur_x.items())))
+    print("  dur by cu-in-sa: " + " ".join(f"{k}:{sum(v)/len(v):.1f}/{max(v):.1f}" for k, v in sorted(dur_cu.items())))
+    print("  dur by (se,sa): " + " ".join(f"{k[0]}{k[1]}:{sum(v)/len(v):.1f}(n{len(v)})" for k, v in sorted(dur_se.items())))
