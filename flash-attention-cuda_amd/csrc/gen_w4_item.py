@@ -77,7 +77,10 @@ def set_dtype(bf16):
               if bf16 else {"mfma": "v_mfma_f32_16x16x32_f16", "cvt_pk": "v_cvt_pk_f16_f32",
                             "one2": "0x3c003c00"})
     DT["bf16"] = bf16
-V_AHEAD = int(os.environ.get("W4_V_AHEAD", "3"))  # V^T fragments read ahead of the PV MFMAs that use them
+V_AHEAD = int(os.environ.get("W4_V_AHEAD", "3"))
+# causal diagonal tile masked block by block inside phase A (W4_DIAG_FAST=0:
+# the general mask after phase A, for A/B)
+DIAG_FAST = os.environ.get("W4_DIAG_FAST", "1") == "1"  # V^T fragments read ahead of the PV MFMAs that use them
 
 
 def regs(spec):
@@ -455,10 +458,16 @@ def stage_loads(st_set=0):
 # ---------------------------------------------------------------------------
 # program pieces
 # ---------------------------------------------------------------------------
-def phase_a(st, p, with_max):
-    """QK^T(j+1) from kbuf[(j+1)&1] beside cvt P(j), maxima of S(j+1), staging"""
+def phase_a(st, p, with_max, diag=False):
+    """QK^T(j+1) from kbuf[(j+1)&1] beside cvt P(j), maxima of S(j+1), staging.
+    diag: the wave's causal diagonal tile with its keys aligned to its rows
+    (kv0 = qm, a whole tile before kv_hi): 16-row block (b, cb) is all valid
+    below the diagonal (cb < b), all masked above it (cb > b: no MFMAs, the
+    scores set to -inf), and masked per element on it (key 4sg + i > row r16)
+    -- the general mask_last_tile + full_max path, block by block, beside
+    the 40 remaining MFMAs"""
     kb = KBUF[1 - p]
-    chains = [(b, cb) for cb in range(4) for b in range(4)]
+    chains = [(b, cb) for cb in range(4) for b in range(4) if not diag or cb <= b]
     mf = []
     if "tmajor" in XP:
         for cb in range(4):
@@ -480,9 +489,17 @@ def phase_a(st, p, with_max):
             ins = [i for i in ins if isinstance(i, str) or "ds_read_b64_tr" not in i.text]
         gaps.setdefault(k, []).extend(ins)
 
+    n = len(mf)
     # K reads of cb 0 first; the conversions of cb 0's four blocks cover
     # their LDS latency
     put(0, [k_read(t, 0, t, kb) for t in range(4)])
+    if diag:
+        # blocks above the diagonal: P(j) out of them, then -inf
+        above = [(b, cb) for cb in range(4) for b in range(4) if cb > b]
+        for k, (b, cb) in enumerate(above):
+            ins = cvt_block(b, cb)
+            ins += [valu(f"v_mov_b32 {S(b, cb, i)}, {VNINF}", r=[VNINF], w=[S(b, cb, i)]) for i in range(4)]
+            put(5 + 5 * k, ins)
     for x, (b, cb) in enumerate(chains):
         c = cvt_block(b, cb)
         if "nocvt" in XP:
@@ -495,11 +512,17 @@ def phase_a(st, p, with_max):
         else:
             put(4 * x - 1, c[0])
             put(4 * x, c[1])
+        if diag and b == cb:
+            # the diagonal block: key 16cb + 4sg + i is valid iff i <= r16 - 4sg
+            for i in range(4):
+                xr = S(b, cb, i)
+                put(min(4 * x + 8, n), [valu(f"v_cmp_le_i32 vcc, {i}, %[vt]", r=["%[vt]"]),
+                                valu(f"v_cndmask_b32 {xr}, {VNINF}, {xr}, vcc", r=[VNINF, xr], w=[xr])])
         # next cb's K fragments early in this cb's first chain (kspread: one
         # per chain of this cb)
-        if "kspread" in XP and cb < 3:
+        if "kspread" in XP and cb < 3 and not diag:
             put(4 * x + 1, k_read(b, cb + 1, 4 * ((cb + 1) & 1) + b, kb))
-        elif b == 0 and cb < 3:
+        elif b == (cb if diag else 0) and cb < 3:
             for t in range(4):
                 put(4 * x + 1 + t % 3, k_read(t, cb + 1, 4 * ((cb + 1) & 1) + t, kb))
         if with_max and x >= 2 and "nomax" not in XP:
@@ -511,7 +534,7 @@ def phase_a(st, p, with_max):
     # stage traffic: LDS writes in cb 0, loads in cb 1
     if "nostage" not in XP and STAGE2:
         for i, ld in enumerate(stage_loads(1 - p)):
-            put(LD_AT + LD_SP * i, ld)
+            put((10 + 2 * i) if diag else (LD_AT + LD_SP * i), ld)
     if "nostage" not in XP and "stage_a" in XP and not STAGE2:
         sw = stage_writes(p)
         put(0, sw[:1])
@@ -522,11 +545,12 @@ def phase_a(st, p, with_max):
     # the first V^T fragments of PV(j) (V(j) is ready since the last barrier)
     for f in range(V_AHEAD):
         for i, r in enumerate(v_reads(0, f, f, VBUF[p])):
-            put(52 - 3 * (V_AHEAD - 3) + 3 * f + i, r)
+            put(n - 12 - 3 * (V_AHEAD - 3) + 3 * f + i, r)
+    assert max(gaps) <= n, "every filler lands in a gap"
     st.interleave(mf, gaps)
     leftover = []
     if with_max and "nomax" not in XP:
-        for y in (14, 15):
+        for y in (len(chains) - 2, len(chains) - 1):
             by, cby = chains[y]
             leftover += max_block(by, cby, first=False)
     return leftover
@@ -770,12 +794,24 @@ def body(st, p, causal, labels):
     phase_b(st, p, left, dec_gap=6, label_slow=L["slow"][p], label_end=L["end"][p])
     # ---- masked: the wave's last QK (causal diagonal / ragged end) ----
     st.label(L["masked"][p])
-    phase_a(st, p, with_max=False)
-    # kv0 = 64 (j+1): ST0 = kv_hi - kv0 - 1, ST1 = qw - kv0
+    # kv0 = 64 (j+1): ST0 = kv_hi - kv0 - 1, ST1 = qm - kv0
     st.raw(f"s_lshl_b32 {ST1}, {SJ1}, 6")
     st.raw(f"s_sub_i32 {ST0}, %[kvhi], {ST1}")
     st.raw(f"s_sub_i32 {ST0}, {ST0}, 1")
     st.raw(f"s_sub_i32 {ST1}, %[qm], {ST1}")
+    if causal and DIAG_FAST:
+        # ---- aligned causal diagonal (every causal wave's last QK unless the
+        # tile is ragged): masked block by block inside phase A ----
+        st.raw(f"s_cmp_eq_u32 {ST1}, 0")
+        st.branch("s_cbranch_scc0", L["general"][p])
+        st.raw(f"s_cmp_ge_i32 {ST0}, 63")
+        st.branch("s_cbranch_scc0", L["general"][p])
+        left = phase_a(st, p, with_max=True, diag=True)
+        stamp(st, 62)
+        stamp_acc(st, 64, 62, 60)
+        phase_b(st, p, left, dec_gap=6, label_slow=L["slow3"][p], label_end=L["end"][p])
+        st.label(L["general"][p])
+    phase_a(st, p, with_max=False)
     mask_last_tile(st, causal)
     full_max(st)
     phase_b(st, p, [], dec_gap=0, label_slow=L["slow2"][p], label_end=L["end"][p])
@@ -1017,7 +1053,7 @@ def epilogue(st, split):
 def generate(causal, split=False):
     st = Stream()
     labels = {k: [newlabel(f"{k}{p}") for p in range(2)]
-              for k in ("loop", "notsteady", "masked", "slow", "slow2", "end")}
+              for k in ("loop", "notsteady", "masked", "general", "slow", "slow2", "slow3", "end")}
     labels["done"] = newlabel("done")
     prologue(st, causal)
     # ST1 = qw * 256 for the epilogue (row base), kept in ST1 after the loop
