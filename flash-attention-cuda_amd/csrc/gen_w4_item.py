@@ -80,7 +80,9 @@ def set_dtype(bf16):
 V_AHEAD = int(os.environ.get("W4_V_AHEAD", "3"))
 # causal diagonal tile masked block by block inside phase A (W4_DIAG_FAST=0:
 # the general mask after phase A, for A/B)
-DIAG_FAST = os.environ.get("W4_DIAG_FAST", "1") == "1"  # V^T fragments read ahead of the PV MFMAs that use them
+DIAG_FAST = os.environ.get("W4_DIAG_FAST", "1") == "1"
+# next item's loads issued before (1) or after (0) the last iteration's PV drain
+PF_BEFORE_DRAIN = os.environ.get("W4_PF_BEFORE", "0") == "1"  # V^T fragments read ahead of the PV MFMAs that use them
 
 
 def regs(spec):
@@ -350,6 +352,12 @@ SJ, SJ1 = "s50", "s51"       # j, j+1
 SNW, SNW1 = "s52", "s53"     # n_w, n_w - 1
 SMASKJ = "s54"               # j+2 == n_w and the wave's last tile needs a mask
 ST0, ST1 = "s55", "s56"
+# item state (the item loop runs inside the asm: fa_w4_kernel.hpp's item
+# table in LDS, 16 dwords per item, read at each item start)
+RQ, RO, RL = "s[72:75]", "s[76:79]", "s[80:83]"   # Q / O of the head, split: LSE rows
+NX = "s[84:87]"             # scratch descriptor for the next item's prefetch
+QW, QM, NTILES, KVHI = "s88", "s89", "s90", "s91"  # this wave's first row, mask coordinate
+ITEM, WARM = "s92", "s93"   # item index; 1 if this item's Q, K(0), V(0), K(1) were prefetched
 
 
 def k_read(t, cb, slot, kb):
@@ -796,9 +804,9 @@ def body(st, p, causal, labels):
     st.label(L["masked"][p])
     # kv0 = 64 (j+1): ST0 = kv_hi - kv0 - 1, ST1 = qm - kv0
     st.raw(f"s_lshl_b32 {ST1}, {SJ1}, 6")
-    st.raw(f"s_sub_i32 {ST0}, %[kvhi], {ST1}")
+    st.raw(f"s_sub_i32 {ST0}, {KVHI}, {ST1}")
     st.raw(f"s_sub_i32 {ST0}, {ST0}, 1")
-    st.raw(f"s_sub_i32 {ST1}, %[qm], {ST1}")
+    st.raw(f"s_sub_i32 {ST1}, {QM}, {ST1}")
     if causal and DIAG_FAST:
         # ---- aligned causal diagonal (every causal wave's last QK unless the
         # tile is ragged): masked block by block inside phase A ----
@@ -817,6 +825,8 @@ def body(st, p, causal, labels):
     phase_b(st, p, [], dec_gap=0, label_slow=L["slow2"][p], label_end=L["end"][p])
     # ---- drain (j = n_w - 1: PV only) / idle (j >= n_w: staging only) ----
     st.label(L["notsteady"][p])
+    st.raw(f"s_cmp_eq_u32 {SJ1}, {NTILES}")
+    st.branch("s_cbranch_scc1", L["last"][p])
     if STAGE2:
         for ins in stage_loads(1 - p) + stage_writes(p):
             st.emit(ins)
@@ -830,12 +840,50 @@ def body(st, p, causal, labels):
             for c in cvt_block(b, cb):
                 st.emit(c)
     pv_plain(st, p)
+    st.branch("s_branch", L["end"][p])
+    # ---- the item's last iteration: no staging (its tiles lie past the
+    # item); with a next item, its Q, K(0), V(0), K(1) are loaded into the
+    # registers the prologue would load them into, once the drain's
+    # conversions have freed the S registers
+    st.label(L["last"][p])
+    nopf, drain_pf, done_pf = newlabel("nopf"), newlabel("drainpf"), newlabel("donepf")
+    st.raw(f"s_mov_b32 {WARM}, 0")
+    st.raw(f"s_add_u32 {ST0}, {ITEM}, 1")
+    st.raw(f"s_cmp_lt_u32 {ST0}, %[nitems]")
+    st.branch("s_cbranch_scc0", nopf)
+    st.raw(f"s_mov_b32 {WARM}, 1")
+    st.raw(f"s_cmp_lt_u32 {SJ}, {SNW}")
+    st.branch("s_cbranch_scc1", drain_pf)
+    prefetch_next(st)
+    st.branch("s_branch", L["end"][p])
+    st.label(drain_pf)
+    for b in range(4):
+        for cb in range(4):
+            for c in cvt_block(b, cb):
+                st.emit(c)
+    if PF_BEFORE_DRAIN:
+        prefetch_next(st)
+        pv_plain(st, p)
+    else:
+        # the drain's PV first: its MFMAs would otherwise queue behind the
+        # prefetch's vector-memory issue
+        pv_plain(st, p)
+        prefetch_next(st)
+    st.branch("s_branch", L["end"][p])
+    st.label(nopf)
+    st.raw(f"s_cmp_lt_u32 {SJ}, {SNW}")
+    st.branch("s_cbranch_scc0", L["end"][p])
+    for b in range(4):
+        for cb in range(4):
+            for c in cvt_block(b, cb):
+                st.emit(c)
+    pv_plain(st, p)
     st.label(L["end"][p], drain_lgkm=True)
     st.raw("s_barrier")
     stamp(st, 62)
     stamp_acc(st, 66, 62, 60)
     st.raw(f"s_add_u32 {SJ}, {SJ}, 1")
-    st.raw(f"s_cmp_lt_u32 {SJ}, %[ntiles]")
+    st.raw(f"s_cmp_lt_u32 {SJ}, {NTILES}")
     if p == 0:
         st.branch("s_cbranch_scc0", L["done"])
     else:
@@ -848,6 +896,120 @@ def pstamp(st, dst):
         st.raw(f"s_memtime s[{dst}:{dst + 1}]")
         st.raw("s_waitcnt lgkmcnt(0)")
         st.lgkm = []
+
+
+def slot_read(st, item_sgpr, dst0):
+    """the 16-dword table slot of item `item_sgpr` into v[dst0:dst0+15]"""
+    st.raw(f"s_lshl_b32 {ST0}, {item_sgpr}, 6")
+    st.raw(f"s_add_u32 {ST0}, {ST0}, %[tab]")
+    st.raw(f"v_mov_b32 {T[0]}, {ST0}")
+    for i in range(4):
+        st.raw(f"ds_read_b128 {R('v', dst0 + 4 * i, 4)}, {T[0]} offset:{16 * i}")
+    st.raw("s_waitcnt lgkmcnt(0)")
+
+
+def rsrc(st, dst, lo, hi, records):
+    """buffer descriptor s[dst:dst+3] from base (lo, hi) and num_records"""
+    st.raw(f"s_mov_b32 s{dst}, {lo}")
+    st.raw(f"s_and_b32 s{dst + 1}, {hi}, 0xffff")
+    st.raw(f"s_mov_b32 s{dst + 2}, {records}")
+    st.raw(f"s_mov_b32 s{dst + 3}, 0x20000")
+
+
+# item table slot (fa_w4_kernel.hpp W4Slot): 0-1 Q head, 2-3 K head (+k0
+# rows), 4-5 V head (+k0 rows), 6-7 O rows base, 8 K/V bytes, 9 q0,
+# 10 tiles, 11 key bound, 12 k0, 13 O bytes, 14-15 LSE rows base
+def read_item(st, causal):
+    """this item's scalars from its table slot, and this wave's row range,
+    tile count n_w and last-tile mask flag (the C++ W4Item of round 2)"""
+    slot_read(st, ITEM, 128)
+    rl = lambda i: f"v{128 + i}"
+    for dst, i in ((40, 2), (41, 3), (44, 4), (45, 5), (ST0, 0), (ST1, 1)):
+        st.raw(f"v_readfirstlane_b32 {dst if isinstance(dst, str) else 's%d' % dst}, {rl(i)}")
+    rsrc(st, 72, ST0, ST1, "%[qrec]")                     # RQ
+    st.raw("v_readfirstlane_b32 s42, v136")                # K/V bytes
+    st.raw("s_and_b32 s41, s41, 0xffff")
+    st.raw("s_mov_b32 s43, 0x20000")
+    st.raw("s_and_b32 s45, s45, 0xffff")
+    st.raw("s_mov_b32 s46, s42")
+    st.raw("s_mov_b32 s47, 0x20000")
+    st.raw(f"v_readfirstlane_b32 {ST0}, v134")
+    st.raw(f"v_readfirstlane_b32 {ST1}, v135")
+    st.raw("v_readfirstlane_b32 s57, v141")               # O bytes
+    rsrc(st, 76, ST0, ST1, "s57")                          # RO
+    st.raw(f"v_readfirstlane_b32 {ST0}, v142")
+    st.raw(f"v_readfirstlane_b32 {ST1}, v143")
+    st.raw("s_lshr_b32 s57, s57, 6")                      # LSE bytes = O bytes / 64
+    rsrc(st, 80, ST0, ST1, "s57")                          # RL
+    st.raw(f"v_readfirstlane_b32 {QW}, v137")             # q0
+    st.raw(f"s_add_u32 {QW}, {QW}, %[woff]")              # + 64 wave
+    st.raw(f"v_readfirstlane_b32 {NTILES}, v138")
+    st.raw(f"v_readfirstlane_b32 {KVHI}, v139")
+    st.raw(f"v_readfirstlane_b32 {ST0}, v140")            # k0
+    st.raw(f"s_sub_i32 {QM}, {QW}, {ST0}")
+    # n_w = causal ? max(0, min(tiles, (qm >> 6) + 1)) : tiles
+    if causal:
+        st.raw(f"s_ashr_i32 {SNW}, {QM}, 6")
+        st.raw(f"s_add_i32 {SNW}, {SNW}, 1")
+        st.raw(f"s_min_i32 {SNW}, {SNW}, {NTILES}")
+        st.raw(f"s_max_i32 {SNW}, {SNW}, 0")
+    else:
+        st.raw(f"s_mov_b32 {SNW}, {NTILES}")
+    st.raw(f"s_sub_u32 {SNW1}, {SNW}, 1")
+    # the wave's last tile (key kv0 = 64 (n_w - 1)) needs a mask iff it
+    # reaches the key bound or (causal) the diagonal: SMASKJ = n_w, else never
+    st.raw(f"s_lshl_b32 {ST0}, {SNW}, 6")                 # kv0 + 64
+    st.raw(f"s_cmp_gt_i32 {ST0}, {KVHI}")
+    st.raw(f"s_cselect_b32 {ST1}, 1, 0")
+    if causal:
+        st.raw(f"s_sub_i32 {ST0}, {ST0}, 1")
+        st.raw(f"s_cmp_gt_i32 {ST0}, {QM}")
+        st.raw(f"s_cselect_b32 {ST0}, 1, 0")
+        st.raw(f"s_or_b32 {ST1}, {ST1}, {ST0}")
+    st.raw(f"s_cmp_eq_u32 {ST1}, 0")
+    st.raw(f"s_cselect_b32 {SMASKJ}, -1, {SNW}")
+    st.nop(5)  # VALU-written descriptor words (readfirstlane) -> buffer loads
+
+
+def prefetch_next(st):
+    """the next item's Q rows (this wave's 64) into v0-63, K(0) into v112..,
+    V(0) and K(1) into staging set 1 -- the cold prologue's loads, issued in
+    this item's last iteration (plain loads: ~10 cycles of issue each, where
+    LDS-DMA pieces cost ~100); their latency hides under the PV drain, the
+    epilogue and the next item's table read"""
+    slot_read(st, f"{ST0}", 112)   # ST0 = ITEM + 1 (set by the caller)
+    st.raw(f"v_readfirstlane_b32 {ST0}, v112")
+    st.raw(f"v_readfirstlane_b32 {ST1}, v113")
+    rsrc(st, 84, ST0, ST1, "%[qrec]")
+    st.raw(f"v_readfirstlane_b32 {ST0}, v121")            # next q0
+    st.raw(f"s_add_u32 {ST0}, {ST0}, %[woff]")
+    st.raw(f"s_lshl_b32 {ST0}, {ST0}, 8")
+    st.raw(f"v_readfirstlane_b32 s57, v120")              # next K/V bytes
+    st.raw(f"v_readfirstlane_b32 s94, v114")               # next K base
+    st.raw(f"v_readfirstlane_b32 s95, v115")
+    st.raw(f"v_readfirstlane_b32 s96, v116")               # next V base
+    st.raw(f"v_readfirstlane_b32 s97, v117")
+    for b in range(4):
+        st.raw(f"v_add_u32 {T[b]}, {ST0}, %[qoff]")
+        if b:
+            st.raw(f"v_add_u32 {T[b]}, {4096 * b}, {T[b]}")
+    st.nop(4)
+    for b in range(4):
+        for t in range(4):
+            st.raw(f"buffer_load_dwordx4 {R('v', 16 * b + 4 * t, 4)}, {T[b]}, {NX}, 0 offen offset:{64 * t}")
+    rsrc(st, 84, "s94", "s95", "s57")
+    st.nop(4)
+    for i in range(4):
+        st.raw(f"buffer_load_dwordx4 {R('v', 112 + 4 * i, 4)}, {KOFF[i]}, {NX}, 0 offen")
+    for i in range(4):
+        st.raw(f"v_add_u32 {T[4 + i]}, 0x4000, {KOFF[i]}")
+    st.nop(1)
+    for i in range(4):
+        st.raw(f"buffer_load_dwordx4 {kst(i, 1)}, {T[4 + i]}, {NX}, 0 offen")
+    rsrc(st, 84, "s96", "s97", "s57")
+    st.nop(4)
+    for i in range(4):
+        st.raw(f"buffer_load_dwordx4 {vst(i, 1)}, {VOFF[i]}, {NX}, 0 offen")
 
 
 def stage0(st):
@@ -909,28 +1071,25 @@ def prologue(st, causal):
     loop -- the DMA issue cost -- and was dropped:
     profiles/r03_ab_w4_next_item_dma.jsonl.)"""
     pstamp(st, 60)
-    st.raw("s_mov_b32 s40, %[rk0]")
-    st.raw("s_mov_b32 s41, %[rk1]")
-    st.raw("s_mov_b32 s42, %[rk2]")
-    st.raw("s_mov_b32 s43, %[rk3]")
-    st.raw("s_mov_b32 s44, %[rv0]")
-    st.raw("s_mov_b32 s45, %[rv1]")
-    st.raw("s_mov_b32 s46, %[rv2]")
-    st.raw("s_mov_b32 s47, %[rv3]")
-    st.raw(f"s_mov_b32 {SNW}, %[nw]")
-    st.raw(f"s_sub_u32 {SNW1}, {SNW}, 1")
-    # SMASKJ = n_w if the last tile needs a mask, else never
-    st.raw(f"s_cmp_eq_u32 %[masklast], 0")
-    st.raw(f"s_cselect_b32 {SMASKJ}, -1, {SNW}")
-    st.nop(4)  # SALU-written descriptors -> buffer loads below
     st.raw(f"v_mov_b32 {VNINF}, {NINF}")
     for i in range(4):
         st.raw(f"v_mov_b32 v{208 + i}, {DT['one2']}")
     for i in range(1, 4):
         st.raw(f"v_add_u32 {KOFF[i]}, {4096 * i}, %[koff]")
         st.raw(f"v_add_u32 {VOFF[i]}, {4096 * i}, %[voff]")
+    cold, join = newlabel("cold"), newlabel("join")
+    st.raw(f"s_cmp_eq_u32 {WARM}, 0")
+    st.branch("s_cbranch_scc1", cold)
+    # ---- warm: Q, K(0), V(0), K(1) were loaded in the previous item's last
+    # iteration (older than its 16 O stores)
+    stage0(st)
+    zero_state(st)
+    st.raw("s_waitcnt vmcnt(24)")
+    st.branch("s_branch", join)
+    # ---- cold: the chunk's first item
+    st.label(cold)
     # Q rows qw + 16b + r16: offset (qw + 16b) * 256 + %[qoff]
-    st.raw(f"s_lshl_b32 {ST0}, %[qw], 8")
+    st.raw(f"s_lshl_b32 {ST0}, {QW}, 8")
     for b in range(4):
         st.raw(f"v_add_u32 {T[b]}, {ST0}, %[qoff]")
         if b:
@@ -938,7 +1097,7 @@ def prologue(st, causal):
     st.nop(1)
     for b in range(4):
         for t in range(4):
-            st.raw(f"buffer_load_dwordx4 {R('v', 16 * b + 4 * t, 4)}, {T[b]}, %[rq], 0 offen offset:{64 * t}")
+            st.raw(f"buffer_load_dwordx4 {R('v', 16 * b + 4 * t, 4)}, {T[b]}, {RQ}, 0 offen offset:{64 * t}")
     # K(0) -> v112.., then V(0) and K(1) into staging set 1 (a224.., a208..:
     # free until iteration 0's loads), waited for only after S(0)
     for i in range(4):
@@ -954,6 +1113,7 @@ def prologue(st, causal):
     zero_state(st)
     # Q and K(0) landed (V(0), K(1) and stage 0 may still fly)
     st.raw("s_waitcnt vmcnt(16)")
+    st.label(join)
     for i in range(4):
         st.raw(f"ds_write_b128 %[klds], {R('v', 112 + 4 * i, 4)} offset:{KBUF[0] + 4096 * i}")
     q_scale(st)
@@ -965,8 +1125,8 @@ def prologue(st, causal):
     st.raw(f"s_cmp_eq_u32 {SMASKJ}, 1")
     skip = newlabel("nomask0")
     st.branch("s_cbranch_scc0", skip)
-    st.raw(f"s_sub_i32 {ST0}, %[kvhi], 1")
-    st.raw(f"s_mov_b32 {ST1}, %[qm]")
+    st.raw(f"s_sub_i32 {ST0}, {KVHI}, 1")
+    st.raw(f"s_mov_b32 {ST1}, {QM}")
     mask_last_tile(st, causal)
     st.label(skip)
     slow_softmax(st, first=True)
@@ -993,7 +1153,7 @@ def epilogue(st, split):
     partial O goes to the workspace slab (%[ro] points there) and the row's
     log2-sum-exp, m_ref + log2(l), to %[rl] (4-B sc1 stores), for the merge"""
     if split:
-        st.raw(f"s_lshl_b32 s57, %[qw], 2")
+        st.raw(f"s_lshl_b32 s57, {QW}, 2")
         st.nop(1)
         st.emit(valu(f"v_lshlrev_b32 {T[9]}, 2, %[r16]", r=["%[r16]"], w=[T[9]]))
         st.emit(valu(f"v_add_u32 {T[9]}, s57, {T[9]}", r=[T[9]], w=[T[9]]))
@@ -1019,14 +1179,14 @@ def epilogue(st, split):
             st.emit(valu(f"v_log_f32_e32 {T[8]}, {l}", r=[l], w=[T[8]], kind="trans"))
             st.emit(valu(f"v_add_f32_e32 {T[8]}, {MREF[b]}, {T[8]}", r=[MREF[b], T[8]], w=[T[8]]))
             st.emit(valu(f"v_add_u32 {T[10]}, {64 * b}, {T[9]}", r=[T[9]], w=[T[10]]))
-            st.emit(vmem(f"buffer_store_dword {T[8]}, {T[10]}, %[rl], 0 offen sc1", r=[T[8], T[10]]))
+            st.emit(vmem(f"buffer_store_dword {T[8]}, {T[10]}, {RL}, 0 offen sc1", r=[T[8], T[10]]))
             st.nop(2)
         # row offset: (qw + 16b + r16) * 256 + 2 * dlane
         st.emit(valu(f"v_add_u32 {T[7]}, {ST1}, %[ooff]", r=["%[ooff]"], w=[T[7]]))
         if b:
             st.emit(valu(f"v_add_u32 {T[7]}, {4096 * b}, {T[7]}", r=[T[7]], w=[T[7]]))
         for ep in range(4):
-            d = [f"v{128 + i}" for i in range(8)]  # O staging: the (free) K fragment slots
+            d = [f"v{144 + i}" for i in range(8)]  # O staging: the (free) V^T fragment slots
             for x in range(2):
                 e = 2 * ep + x
                 for i in range(4):
@@ -1036,16 +1196,16 @@ def epilogue(st, split):
                     continue
                 for i in range(4):
                     st.emit(valu(f"v_mul_f32_e32 {d[4 * x + i]}, {d[4 * x + i]}, {inv}", r=[d[4 * x + i], inv], w=[d[4 * x + i]]))
-            # X = e even pair -> v120,121 ; Y = e odd -> v122,123
-            X, Y = ["v120", "v121"], ["v122", "v123"]
+            # X = e even pair -> v152,153 ; Y = e odd -> v154,155
+            X, Y = ["v152", "v153"], ["v154", "v155"]
             st.emit(valu(f"{DT['cvt_pk']} {X[0]}, {d[0]}, {d[1]}", r=d[0:2], w=[X[0]]))
             st.emit(valu(f"{DT['cvt_pk']} {X[1]}, {d[2]}, {d[3]}", r=d[2:4], w=[X[1]]))
             st.emit(valu(f"{DT['cvt_pk']} {Y[0]}, {d[4]}, {d[5]}", r=d[4:6], w=[Y[0]]))
             st.emit(valu(f"{DT['cvt_pk']} {Y[1]}, {d[6]}, {d[7]}", r=d[6:8], w=[Y[1]]))
             for dw in range(2):
                 st.emit(valu(f"v_permlane16_swap_b32 {X[dw]}, {Y[dw]}", r=[X[dw], Y[dw]], w=[X[dw], Y[dw]]))
-            st.emit(vmem(f"buffer_store_dwordx4 v[120:123], {T[7]}, %[ro], 0 offen offset:{64 * ep} sc1",
-                         r=["v[120:123]", T[7]]))
+            st.emit(vmem(f"buffer_store_dwordx4 v[152:155], {T[7]}, {RO}, 0 offen offset:{64 * ep} sc1",
+                         r=["v[152:155]", T[7]]))
             st.nop(2)
     st.nop(2)
 
@@ -1054,14 +1214,23 @@ def generate(causal, split=False):
     st = Stream()
     labels = {k: [newlabel(f"{k}{p}") for p in range(2)]
               for k in ("loop", "notsteady", "masked", "general", "slow", "slow2", "slow3", "end")}
+    labels["last"] = [newlabel(f"last{p}") for p in range(2)]
     labels["done"] = newlabel("done")
+    item = newlabel("item")
+    # the workgroup's items (a chunk of fa_w4_kernel.hpp's table) in one
+    # statement, so the next item's operands can be loaded in this one's
+    # last iteration
+    st.raw(f"s_mov_b32 {ITEM}, 0")
+    st.raw(f"s_mov_b32 {WARM}, 0")
+    st.label(item)
+    read_item(st, causal)
     prologue(st, causal)
-    # ST1 = qw * 256 for the epilogue (row base), kept in ST1 after the loop
     body(st, 0, causal, labels)
     body(st, 1, causal, labels)
     st.label(labels["done"], drain_lgkm=True)
     pstamp(st, 64)
-    st.raw(f"s_lshl_b32 {ST1}, %[qw], 8")
+    # ST1 = qw * 256: the epilogue's row base
+    st.raw(f"s_lshl_b32 {ST1}, {QW}, 8")
     st.nop(1)
     epilogue(st, split)
     if DIAG == "pstamps":
@@ -1075,7 +1244,7 @@ def generate(causal, split=False):
             st.raw(f"v_mov_b32 v{120 + i}, s57")
         st.raw(f"v_mov_b32 v124, s{ST1[1:]}")
         st.nop(2)
-        st.raw("buffer_store_dwordx4 v[120:123], v124, %[ro], 0 offen")
+        st.raw(f"buffer_store_dwordx4 v[120:123], v124, {RO}, 0 offen")
         st.nop(2)
     if DIAG == "stamps":
         # [phase A, phase B, barrier (wait + skew), steady iterations] of
@@ -1084,8 +1253,11 @@ def generate(causal, split=False):
             st.raw(f"v_mov_b32 v{120 + i}, s{r}")
         st.raw(f"v_mov_b32 v124, s{ST1[1:]}")
         st.nop(2)
-        st.raw("buffer_store_dwordx4 v[120:123], v124, %[ro], 0 offen")
+        st.raw(f"buffer_store_dwordx4 v[120:123], v124, {RO}, 0 offen")
         st.nop(2)
+    st.raw(f"s_add_u32 {ITEM}, {ITEM}, 1")
+    st.raw(f"s_cmp_lt_u32 {ITEM}, %[nitems]")
+    st.branch("s_cbranch_scc1", item)
     return st.out
 
 
@@ -1100,19 +1272,16 @@ def cxx(causal, bf16, lines, split=False):
     body = "\n".join(f'      "{l}\\n"' for l in lines)
     vclob = ", ".join(f'"v{i}"' for i in range(236))
     aclob = ", ".join(f'"a{i}"' for i in range(240 if STAGE2 else 208))
-    sclob = ", ".join(f'"s{i}"' for i in range(40, 70 if DIAG in ("stamps", "pstamps") else 60))
+    sclob = ", ".join(f'"s{i}"' for i in range(40, 98))
     name = (("w4_item_causal" if causal else "w4_item_noncausal") + ("_split" if split else "")
             + ("_bf16" if bf16 else "_f16"))
     return f"""
-__device__ __forceinline__ void {name}(const W4Item& it, const W4Lane& ln) {{
+__device__ __forceinline__ void {name}(const W4Run& rn, const W4Lane& ln) {{
   asm volatile(
 {body}
       :
-      : [rq] "s"(it.rq), [ro] "s"(it.ro),
-        [rk0] "s"(it.rk0), [rk1] "s"(it.rk1), [rk2] "s"(it.rk2), [rk3] "s"(it.rk3),
-        [rv0] "s"(it.rv0), [rv1] "s"(it.rv1), [rv2] "s"(it.rv2), [rv3] "s"(it.rv3),
-        [qw] "s"(it.qw), [qm] "s"(it.qm), [rl] "s"(it.rl), [ntiles] "s"(it.ntiles), [nw] "s"(it.nw), [masklast] "s"(it.masklast),
-        [kvhi] "s"(it.kvhi), [c] "s"(it.c),
+      : [tab] "s"(rn.tab), [nitems] "s"(rn.nitems), [woff] "s"(rn.woff), [qrec] "s"(rn.qrec),
+        [c] "s"(rn.c),
         [ka0] "v"(ln.ka[0]), [ka1] "v"(ln.ka[1]), [ka2] "v"(ln.ka[2]), [ka3] "v"(ln.ka[3]),
         [va0] "v"(ln.va[0]), [va1] "v"(ln.va[1]), [koff] "v"(ln.koff), [voff] "v"(ln.voff),
         [klds] "v"(ln.klds), [vlds] "v"(ln.vlds), [vt] "v"(ln.vt), [r16] "v"(ln.r16),
