@@ -1045,16 +1045,19 @@ def q_scale(st):
         lo = {x: f"v{144 + 3 * (x - x0)}" for x in xs}
         hi = {x: f"v{145 + 3 * (x - x0)}" for x in xs}
         pk = {x: f"v{146 + 3 * (x - x0)}" for x in xs}
-        for x in xs:
-            if DT["bf16"]:  # bf16 -> fp32 is exact: the 16 bits move to the top half
+        if DT["bf16"]:
+            for x in xs:  # bf16 -> fp32 is exact: the 16 bits move to the top half
                 st.raw(f"v_lshlrev_b32_e32 {lo[x]}, 16, v{x}")
                 st.raw(f"v_and_b32_e32 {hi[x]}, 0xffff0000, v{x}")
-            else:
-                st.raw(f"v_cvt_f32_f16_e32 {lo[x]}, v{x}")
-                st.raw(f"v_cvt_f32_f16_sdwa {hi[x]}, v{x} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1")
-        for x in xs:
-            st.raw(f"v_mul_f32_e32 {lo[x]}, %[c], {lo[x]}")
-            st.raw(f"v_mul_f32_e32 {hi[x]}, %[c], {hi[x]}")
+            for x in xs:
+                st.raw(f"v_mul_f32_e32 {lo[x]}, %[c], {lo[x]}")
+                st.raw(f"v_mul_f32_e32 {hi[x]}, %[c], {hi[x]}")
+        else:
+            # fp16 half * c in one mixed-precision fma: fma(q, c, -0) is the
+            # fp32 product rounded once (= cvt + v_mul_f32, signed zeros too)
+            for x in xs:
+                st.raw(f"v_fma_mix_f32 {lo[x]}, v{x}, %[c], neg(0) op_sel_hi:[1,0,0]")
+                st.raw(f"v_fma_mix_f32 {hi[x]}, v{x}, %[c], neg(0) op_sel:[1,0,0] op_sel_hi:[1,0,0]")
         for x in xs:
             st.raw(f"{DT['cvt_pk']} {pk[x]}, {lo[x]}, {hi[x]}")
         for x in xs:
