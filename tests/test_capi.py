@@ -322,3 +322,24 @@ def test_split_plan_and_workspace_entry():
     assert lib.fa_fwd_bf16_ws(p, p, p, p, 1, 4, 4096, 96, 1, 0, p, need, None) == \
         fa.FA_ERR_UNSUPPORTED_HEAD_DIM
     assert lib.fa_fwd_f16_ws(None, p, p, p, 1, 4, 4096, 128, 1, 0, p, need, None) == fa.FA_ERR_NULL_POINTER
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")
+def test_no_kernel_uses_scratch():
+    """Compile-time twin of test_fullsize_gpu.test_register_report: every
+    kernel of the library -- the asm item programs included, whose statement
+    leaves hipcc 20 VGPRs for whatever is live across it -- keeps all of its
+    state in registers (ScratchSize 0), checked from hipcc's resource-usage
+    remarks so a spill is caught without a GPU."""
+    pkg = os.path.join(ROOT, "flash-attention-cuda_amd")
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-honor-nans",
+           "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(pkg, "csrc"), "-c",
+           os.path.join(pkg, "csrc", "fa_fwd.hip"), "-o", os.devnull,
+           "-Rpass-analysis=kernel-resource-usage"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    names = re.findall(r"Function Name: (\S+)", out.stderr)
+    scratch = [int(x) for x in re.findall(r"ScratchSize \[bytes/lane\]: (\d+)", out.stderr)]
+    assert names and len(names) == len(scratch), (len(names), len(scratch))
+    spills = {n: s for n, s in zip(names, scratch) if s}
+    assert not spills, spills
