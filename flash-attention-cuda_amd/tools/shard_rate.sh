@@ -5,5 +5,5 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}/flash-attention-cuda_amd" || exit 1
 mkdir -p ../gpurun_out
 for b in 64 32 16 8; do
-  timeout -k 10 200 python tools/ab.py --configs 7 --seq 4096 --batch $b --causal --rounds 5 --iters $((320 / b)) || exit 1
+  timeout -k 10 200 python tools/ab.py --configs auto --seq 4096 --batch $b --causal --rounds 5 --iters $((320 / b)) || exit 1
 done > ../gpurun_out/shard_rate.jsonl 2>&1
