@@ -343,3 +343,19 @@ def test_no_kernel_uses_scratch():
     assert names and len(names) == len(scratch), (len(names), len(scratch))
     spills = {n: s for n, s in zip(names, scratch) if s}
     assert not spills, spills
+
+
+def test_generated_item_program_is_current(tmp_path):
+    """The committed asm item program (csrc/fa_w4_item.inc) is exactly what
+    csrc/gen_w4_item.py generates: the Makefile regenerates it by mtime only,
+    so after a checkout a stale include could otherwise be compiled."""
+    import sys
+
+    csrc = os.path.join(ROOT, "flash-attention-cuda_amd", "csrc")
+    out = tmp_path / "fa_w4_item.inc"
+    env = {k: v for k, v in os.environ.items() if not k.startswith("W4_")}  # no experiment knobs
+    subprocess.run([sys.executable, os.path.join(csrc, "gen_w4_item.py"), str(out)], check=True,
+                   env=env, timeout=300)
+    with open(os.path.join(csrc, "fa_w4_item.inc")) as f:
+        committed = f.read()
+    assert out.read_text() == committed, "fa_w4_item.inc is stale: run `make -C flash-attention-cuda_amd`"
