@@ -83,6 +83,12 @@ V_AHEAD = int(os.environ.get("W4_V_AHEAD", "3"))
 DIAG_FAST = os.environ.get("W4_DIAG_FAST", "1") == "1"
 # next item's loads issued before (1) or after (0) the last iteration's PV drain
 PF_BEFORE_DRAIN = os.environ.get("W4_PF_BEFORE", "0") == "1"  # V^T fragments read ahead of the PV MFMAs that use them
+# cross-item overlap (non-split programs): an item with a successor defers
+# its epilogue (O read-out, 1/l scaling, fp16 conversion, stores) into the
+# successor's prologue, beside the S(0) QK^T MFMAs, which touch no O
+# register; its O descriptor and row base wait in s[60:63] / s64
+XOVL = os.environ.get("W4_XOVL", "1") == "1" and DIAG not in ("stamps", "pstamps")  # (s60-s69: stamps)
+ROSAVE, ROWSAVE = "s[60:63]", "s64"
 
 
 def regs(spec):
@@ -1064,7 +1070,7 @@ def q_scale(st):
             st.raw(f"v_accvgpr_write_b32 a{144 + x}, {pk[x]}")
 
 
-def prologue(st, causal):
+def prologue(st, causal, split=False):
     """Q (scaled), K(0), K(1), V(0) into registers / LDS, stage 0 in flight,
     S(0) = K(0) Q^T with the first-tile rescale and exp2.  V(0) and K(1)
     are waited for only after S(0) (their latency under the Q scaling, the
@@ -1084,10 +1090,22 @@ def prologue(st, causal):
     st.raw(f"s_cmp_eq_u32 {WARM}, 0")
     st.branch("s_cbranch_scc1", cold)
     # ---- warm: Q, K(0), V(0), K(1) were loaded in the previous item's last
-    # iteration (older than its 16 O stores)
+    # iteration
+    xovl = XOVL and not split
     stage0(st)
-    zero_state(st)
-    st.raw("s_waitcnt vmcnt(24)")
+    if xovl:
+        # O and l still hold the previous item's result (its deferred
+        # epilogue zeroes them); in flight: prefetch (Q 16, K(0) 4, K(1) 4,
+        # V(0) 4) then stage 0 (8): Q and K(0) landed at vmcnt(16)
+        for x in range(96, 112):
+            st.raw(f"v_mov_b32 v{x}, 0")
+        for b in range(4):
+            st.raw(f"v_mov_b32 {MREF[b]}, 0")
+        st.raw("s_waitcnt vmcnt(16)")
+    else:
+        # (older than the previous item's 16 O stores)
+        zero_state(st)
+        st.raw("s_waitcnt vmcnt(24)")
     st.branch("s_branch", join)
     # ---- cold: the chunk's first item
     st.label(cold)
@@ -1124,7 +1142,17 @@ def prologue(st, causal):
     st.raw("s_barrier")
     st.nop(2)
     # S(0)
-    qk_plain(st, KBUF[0])
+    if xovl:
+        cold_s0, s0done = newlabel("colds0"), newlabel("s0done")
+        st.raw(f"s_cmp_eq_u32 {WARM}, 0")
+        st.branch("s_cbranch_scc1", cold_s0)
+        s0_with_epilogue(st)
+        st.branch("s_branch", s0done)
+        st.label(cold_s0)
+        qk_plain(st, KBUF[0])
+        st.label(s0done)
+    else:
+        qk_plain(st, KBUF[0])
     st.raw(f"s_cmp_eq_u32 {SMASKJ}, 1")
     skip = newlabel("nomask0")
     st.branch("s_cbranch_scc0", skip)
@@ -1135,8 +1163,19 @@ def prologue(st, causal):
     slow_softmax(st, first=True)
     for e in exp_ops():
         st.emit(e)
-    # V(0), K(1) landed: into their LDS images
-    st.raw("s_waitcnt vmcnt(8)")
+    # V(0), K(1) landed: into their LDS images (warm with the deferred
+    # epilogue: its 16 O stores are the youngest, behind stage 0's 8 loads)
+    if xovl:
+        cw, cd = newlabel("coldw"), newlabel("waitdone")
+        st.raw(f"s_cmp_eq_u32 {WARM}, 0")
+        st.branch("s_cbranch_scc1", cw)
+        st.raw("s_waitcnt vmcnt(24)")
+        st.branch("s_branch", cd)
+        st.label(cw)
+        st.raw("s_waitcnt vmcnt(8)")
+        st.label(cd)
+    else:
+        st.raw("s_waitcnt vmcnt(8)")
     for i in range(4):
         st.raw(f"ds_write_b128 %[vlds], {vst(i, 1)} offset:{VBUF[0] + 4096 * i}")
         st.raw(f"ds_write_b128 %[klds], {kst(i, 1)} offset:{KBUF[1] + 4096 * i}")
@@ -1150,67 +1189,103 @@ def prologue(st, causal):
             st.raw(f"s_mov_b32 s{r}, 0")
 
 
-def epilogue(st, split):
-    """O / l -> fp16 rows (M16::store_o: permlane16 swaps, dwordx4 stores, sc1).
+def epilogue_ops(split, ro=RO, rowbase=ST1, zero_o=False):
+    """O / l -> fp16 rows (M16::store_o: permlane16 swaps, dwordx4 stores, sc1)
+    as a list of instructions (strings: raw SALU / padding).
     split: the item is one key piece of its query block -- the normalised
     partial O goes to the workspace slab (%[ro] points there) and the row's
-    log2-sum-exp, m_ref + log2(l), to %[rl] (4-B sc1 stores), for the merge"""
+    log2-sum-exp, m_ref + log2(l), to %[rl] (4-B sc1 stores), for the merge.
+    zero_o: each O / l register is zeroed right after it is read (the
+    deferred epilogue runs inside the next item's prologue, which owns them
+    next)."""
+    ops = []
+    E = ops.append
     if split:
-        st.raw(f"s_lshl_b32 s57, {QW}, 2")
-        st.nop(1)
-        st.emit(valu(f"v_lshlrev_b32 {T[9]}, 2, %[r16]", r=["%[r16]"], w=[T[9]]))
-        st.emit(valu(f"v_add_u32 {T[9]}, s57, {T[9]}", r=[T[9]], w=[T[9]]))
+        E(f"s_lshl_b32 s57, {QW}, 2")
+        E("s_nop 0")
+        E(valu(f"v_lshlrev_b32 {T[9]}, 2, %[r16]", r=["%[r16]"], w=[T[9]]))
+        E(valu(f"v_add_u32 {T[9]}, s57, {T[9]}", r=[T[9]], w=[T[9]]))
     for b in range(4):
         l, inv = T[0], T[1]
-        st.emit(valu(f"v_accvgpr_read_b32 {l}, {L(b, 0)}", r=[L(b, 0)], w=[l]))
+        E(valu(f"v_accvgpr_read_b32 {l}, {L(b, 0)}", r=[L(b, 0)], w=[l]))
+        if zero_o:
+            for i in range(4):
+                E(valu(f"v_accvgpr_write_b32 {L(b, i)}, 0", w=[L(b, i)]))
         # inv = l > 0 ? 1.0f / l : 0  (IEEE division, the compiler's sequence)
-        st.emit(valu(f"v_div_scale_f32 {T[2]}, s[58:59], {l}, {l}, 1.0", r=[l], w=[T[2]]))
-        st.emit(valu(f"v_rcp_f32_e32 {T[3]}, {T[2]}", r=[T[2]], w=[T[3]], kind="trans"))
-        st.emit(valu(f"v_fma_f32 {T[4]}, -{T[2]}, {T[3]}, 1.0", r=[T[2], T[3]], w=[T[4]]))
-        st.emit(valu(f"v_fmac_f32_e32 {T[3]}, {T[4]}, {T[3]}", r=[T[3], T[4]], w=[T[3]]))
-        st.emit(valu(f"v_div_scale_f32 {T[4]}, vcc, 1.0, {l}, 1.0", r=[l], w=[T[4]]))
-        st.emit(valu(f"v_mul_f32_e32 {T[5]}, {T[4]}, {T[3]}", r=[T[4], T[3]], w=[T[5]]))
-        st.emit(valu(f"v_fma_f32 {T[6]}, -{T[2]}, {T[5]}, {T[4]}", r=[T[2], T[5], T[4]], w=[T[6]]))
-        st.emit(valu(f"v_fmac_f32_e32 {T[5]}, {T[6]}, {T[3]}", r=[T[5], T[6], T[3]], w=[T[5]]))
-        st.emit(valu(f"v_fma_f32 {T[2]}, -{T[2]}, {T[5]}, {T[4]}", r=[T[2], T[5], T[4]], w=[T[2]]))
-        st.emit(valu(f"v_div_fmas_f32 {T[2]}, {T[2]}, {T[3]}, {T[5]}", r=[T[2], T[3], T[5]], w=[T[2]]))
-        st.emit(valu(f"v_div_fixup_f32 {T[2]}, {T[2]}, {l}, 1.0", r=[T[2], l], w=[T[2]]))
-        st.emit(valu(f"v_cmp_lt_f32 vcc, 0, {l}", r=[l]))
-        st.emit(valu(f"v_cndmask_b32 {inv}, 0, {T[2]}, vcc", r=[T[2]], w=[inv]))
+        E(valu(f"v_div_scale_f32 {T[2]}, s[58:59], {l}, {l}, 1.0", r=[l], w=[T[2]]))
+        E(valu(f"v_rcp_f32_e32 {T[3]}, {T[2]}", r=[T[2]], w=[T[3]], kind="trans"))
+        E(valu(f"v_fma_f32 {T[4]}, -{T[2]}, {T[3]}, 1.0", r=[T[2], T[3]], w=[T[4]]))
+        E(valu(f"v_fmac_f32_e32 {T[3]}, {T[4]}, {T[3]}", r=[T[3], T[4]], w=[T[3]]))
+        E(valu(f"v_div_scale_f32 {T[4]}, vcc, 1.0, {l}, 1.0", r=[l], w=[T[4]]))
+        E(valu(f"v_mul_f32_e32 {T[5]}, {T[4]}, {T[3]}", r=[T[4], T[3]], w=[T[5]]))
+        E(valu(f"v_fma_f32 {T[6]}, -{T[2]}, {T[5]}, {T[4]}", r=[T[2], T[5], T[4]], w=[T[6]]))
+        E(valu(f"v_fmac_f32_e32 {T[5]}, {T[6]}, {T[3]}", r=[T[5], T[6], T[3]], w=[T[5]]))
+        E(valu(f"v_fma_f32 {T[2]}, -{T[2]}, {T[5]}, {T[4]}", r=[T[2], T[5], T[4]], w=[T[2]]))
+        E(valu(f"v_div_fmas_f32 {T[2]}, {T[2]}, {T[3]}, {T[5]}", r=[T[2], T[3], T[5]], w=[T[2]]))
+        E(valu(f"v_div_fixup_f32 {T[2]}, {T[2]}, {l}, 1.0", r=[T[2], l], w=[T[2]]))
+        E(valu(f"v_cmp_lt_f32 vcc, 0, {l}", r=[l]))
+        E(valu(f"v_cndmask_b32 {inv}, 0, {T[2]}, vcc", r=[T[2]], w=[inv]))
         if split:
             # log2(l) + m_ref (-inf for an empty row), row qw + 16b + r16
-            st.emit(valu(f"v_log_f32_e32 {T[8]}, {l}", r=[l], w=[T[8]], kind="trans"))
-            st.emit(valu(f"v_add_f32_e32 {T[8]}, {MREF[b]}, {T[8]}", r=[MREF[b], T[8]], w=[T[8]]))
-            st.emit(valu(f"v_add_u32 {T[10]}, {64 * b}, {T[9]}", r=[T[9]], w=[T[10]]))
-            st.emit(vmem(f"buffer_store_dword {T[8]}, {T[10]}, {RL}, 0 offen sc1", r=[T[8], T[10]]))
-            st.nop(2)
+            E(valu(f"v_log_f32_e32 {T[8]}, {l}", r=[l], w=[T[8]], kind="trans"))
+            E(valu(f"v_add_f32_e32 {T[8]}, {MREF[b]}, {T[8]}", r=[MREF[b], T[8]], w=[T[8]]))
+            E(valu(f"v_add_u32 {T[10]}, {64 * b}, {T[9]}", r=[T[9]], w=[T[10]]))
+            E(vmem(f"buffer_store_dword {T[8]}, {T[10]}, {RL}, 0 offen sc1", r=[T[8], T[10]]))
+            E("s_nop 1")
         # row offset: (qw + 16b + r16) * 256 + 2 * dlane
-        st.emit(valu(f"v_add_u32 {T[7]}, {ST1}, %[ooff]", r=["%[ooff]"], w=[T[7]]))
+        E(valu(f"v_add_u32 {T[7]}, {rowbase}, %[ooff]", r=["%[ooff]"], w=[T[7]]))
         if b:
-            st.emit(valu(f"v_add_u32 {T[7]}, {4096 * b}, {T[7]}", r=[T[7]], w=[T[7]]))
+            E(valu(f"v_add_u32 {T[7]}, {4096 * b}, {T[7]}", r=[T[7]], w=[T[7]]))
         for ep in range(4):
             d = [f"v{144 + i}" for i in range(8)]  # O staging: the (free) V^T fragment slots
             for x in range(2):
                 e = 2 * ep + x
                 for i in range(4):
                     src = L(b, i) if DIAG == "l" else O(b, e, i)
-                    st.emit(valu(f"v_accvgpr_read_b32 {d[4 * x + i]}, {src}", r=[src], w=[d[4 * x + i]]))
+                    E(valu(f"v_accvgpr_read_b32 {d[4 * x + i]}, {src}", r=[src], w=[d[4 * x + i]]))
+                    if zero_o:
+                        E(valu(f"v_accvgpr_write_b32 {O(b, e, i)}, 0", w=[O(b, e, i)]))
                 if DIAG in ("raw", "l"):
                     continue
                 for i in range(4):
-                    st.emit(valu(f"v_mul_f32_e32 {d[4 * x + i]}, {d[4 * x + i]}, {inv}", r=[d[4 * x + i], inv], w=[d[4 * x + i]]))
+                    E(valu(f"v_mul_f32_e32 {d[4 * x + i]}, {d[4 * x + i]}, {inv}", r=[d[4 * x + i], inv], w=[d[4 * x + i]]))
             # X = e even pair -> v152,153 ; Y = e odd -> v154,155
             X, Y = ["v152", "v153"], ["v154", "v155"]
-            st.emit(valu(f"{DT['cvt_pk']} {X[0]}, {d[0]}, {d[1]}", r=d[0:2], w=[X[0]]))
-            st.emit(valu(f"{DT['cvt_pk']} {X[1]}, {d[2]}, {d[3]}", r=d[2:4], w=[X[1]]))
-            st.emit(valu(f"{DT['cvt_pk']} {Y[0]}, {d[4]}, {d[5]}", r=d[4:6], w=[Y[0]]))
-            st.emit(valu(f"{DT['cvt_pk']} {Y[1]}, {d[6]}, {d[7]}", r=d[6:8], w=[Y[1]]))
+            E(valu(f"{DT['cvt_pk']} {X[0]}, {d[0]}, {d[1]}", r=d[0:2], w=[X[0]]))
+            E(valu(f"{DT['cvt_pk']} {X[1]}, {d[2]}, {d[3]}", r=d[2:4], w=[X[1]]))
+            E(valu(f"{DT['cvt_pk']} {Y[0]}, {d[4]}, {d[5]}", r=d[4:6], w=[Y[0]]))
+            E(valu(f"{DT['cvt_pk']} {Y[1]}, {d[6]}, {d[7]}", r=d[6:8], w=[Y[1]]))
             for dw in range(2):
-                st.emit(valu(f"v_permlane16_swap_b32 {X[dw]}, {Y[dw]}", r=[X[dw], Y[dw]], w=[X[dw], Y[dw]]))
-            st.emit(vmem(f"buffer_store_dwordx4 v[152:155], {T[7]}, {RO}, 0 offen offset:{64 * ep} sc1",
-                         r=["v[152:155]", T[7]]))
-            st.nop(2)
-    st.nop(2)
+                E(valu(f"v_permlane16_swap_b32 {X[dw]}, {Y[dw]}", r=[X[dw], Y[dw]], w=[X[dw], Y[dw]]))
+            E(vmem(f"buffer_store_dwordx4 v[152:155], {T[7]}, {ro}, 0 offen offset:{64 * ep} sc1",
+                   r=["v[152:155]", T[7]]))
+            E("s_nop 1")
+    E("s_nop 1")
+    return ops
+
+
+def epilogue(st, split):
+    for op in epilogue_ops(split):
+        st.emit(op)
+
+
+def s0_with_epilogue(st):
+    """S(0) = K(0) Q^T (qk_plain's chains) with the previous item's deferred
+    epilogue (zeroing O and l behind itself) spread over the MFMA gaps"""
+    kb = KBUF[0]
+    mf, gaps = [], {}
+    for cb in range(4):
+        for b in range(4):
+            mf += qk_chain(b, cb, [4 * (cb & 1) + t for t in range(4)])
+    gaps[0] = [k_read(t, 0, t, kb) for t in range(4)]
+    for cb in range(3):
+        for t in range(4):
+            gaps.setdefault(16 * cb + 1 + t, []).append(k_read(t, cb + 1, 4 * ((cb + 1) & 1) + t, kb))
+    ops = epilogue_ops(False, ro=ROSAVE, rowbase=ROWSAVE, zero_o=True)
+    n = len(mf)
+    for i, op in enumerate(ops):
+        gaps.setdefault((i * n) // len(ops), []).append(op)
+    st.interleave(mf, gaps)
 
 
 def generate(causal, split=False):
@@ -1227,11 +1302,23 @@ def generate(causal, split=False):
     st.raw(f"s_mov_b32 {WARM}, 0")
     st.label(item)
     read_item(st, causal)
-    prologue(st, causal)
+    prologue(st, causal, split)
     body(st, 0, causal, labels)
     body(st, 1, causal, labels)
     st.label(labels["done"], drain_lgkm=True)
     pstamp(st, 64)
+    if XOVL and not split:
+        # a successor follows: defer this item's epilogue into its prologue
+        last = newlabel("lastepi")
+        st.raw(f"s_add_u32 {ST0}, {ITEM}, 1")
+        st.raw(f"s_cmp_lt_u32 {ST0}, %[nitems]")
+        st.branch("s_cbranch_scc0", last)
+        for i in range(4):
+            st.raw(f"s_mov_b32 s{60 + i}, s{76 + i}")
+        st.raw(f"s_lshl_b32 {ROWSAVE}, {QW}, 8")
+        st.raw(f"s_mov_b32 {ITEM}, {ST0}")
+        st.raw(f"s_branch {item}")
+        st.label(last)
     # ST1 = qw * 256: the epilogue's row base
     st.raw(f"s_lshl_b32 {ST1}, {QW}, 8")
     st.nop(1)
