@@ -12,22 +12,24 @@ statement whose registers are fixed here:
         v64-95   P, fp16, B operands of PV  (b, u) x 4
         v96-111  -m_ref broadcast per row block (C operand of QK^T chains)
         v112-143 K fragments (8 slots)      v144-175 V^T fragments (8 slots)
-        v176-207 K/V staging registers (one stage in flight)
+        v176-183 per-pass LDS-DMA source offsets of the K/V staging
         v208-235 constants, m_ref, running maxima, temporaries
   AGPR  a0-127   O^T accumulator (b, e) x 4    a128-143 row sums l (b)
         a144-207 Q (pre-scaled by log2(e)/sqrt(d)), B operands of QK^T
+        a208-239 the next item's K(1) / V(0), loaded into registers during
+                 the previous item's last iteration (prologue only)
   the compiler keeps v236-v255 for the lane constants passed in.
 
 Per key tile j (after the prologue computed S(0)) every wave runs
   phase A: QK^T(j+1) -- 64 MFMAs in 16 four-deep chains; beside them the fp16
            conversion of P(j) (each block just before the chain that
            overwrites its registers), the running row maxima of S(j+1), the
-           K reads, and the stage traffic (LDS writes of K(j+2)/V(j+1), global
-           loads of the next stage)
+           K reads, and the stage traffic (LDS-DMA of K(j+2) / V(j+1) straight
+           into the LDS images the previous iteration finished reading)
   phase B: PV(j) + row sums -- 72 MFMAs; beside them the rescale decision
            (wave-uniform branch, rare slow path) and exp2 of S(j+1), one v_exp
            per MFMA gap, and the V^T transposed reads
-  one barrier.
+  s_waitcnt vmcnt(0) (this iteration's DMA landed), one barrier.
 The arithmetic is the M16 policy's (fa_fwd_kernel.hpp) operation for
 operation, per 32-row half (the rescale decision is taken per half, as the
 8-wave ping-pong's 32-row waves take it), so results match the ping-pong
@@ -432,6 +434,28 @@ STAGE2 = "stage1" not in XP
 # 8 descriptor updates)
 LD_AT = int(os.environ.get("W4_LD_AT", "18"))
 LD_SP = int(os.environ.get("W4_LD_SP", "2"))
+DMA_AT = int(os.environ.get("W4_DMA_AT", "2"))  # first phase-A gap of the DMA sequence
+
+
+# K/V staging by LDS-DMA (the default; W4_XP=regstage: the round-3 register
+# staging, for A/B): each wave's 4+4 1-KiB pieces of the
+# next K/V tiles go straight into their LDS images (buffer_load_dwordx4 ...
+# lds, lane-linear destination at M0, per-lane source offsets through the
+# images' inverse swizzle), so phase B carries no ds_writes and no staging
+# registers are needed.  Issued in phase A of iteration j into the buffers
+# iteration j-1 finished reading (K(j+2) -> kbuf[j&1], V(j+1) -> vbuf[(j+1)&1])
+# and waited for (vmcnt(0)) before the iteration's barrier.
+DMA = "regstage" not in XP
+SM0 = "s70"          # M0 of the enclosing code, restored at the end
+SG0 = 0 if DMA else 8  # prologue stage-0 loads in flight (none under DMA)
+
+
+def KD(i):
+    return R("v", 176 + i)   # per-pass K source offsets (DMA)
+
+
+def VD(i):
+    return R("v", 180 + i)   # per-pass V source offsets (DMA)
 
 
 def kst(i, st_set):
@@ -445,6 +469,8 @@ def vst(i, st_set):
 def stage_writes(p):
     """LDS writes of stage j (K(j+2) -> kbuf[j&1], V(j+1) -> vbuf[(j+1)&1]);
     with two sets the 8 youngest loads (stage j+1) may still be in flight"""
+    if DMA:
+        return []
     ss = p if STAGE2 else 0
     out = [f"s_waitcnt vmcnt({8 if STAGE2 else 0})"]
     for i in range(4):
@@ -453,9 +479,46 @@ def stage_writes(p):
     return out
 
 
-def stage_loads(st_set=0):
+def dma_loads(p):
+    """LDS-DMA of K(j+2) -> kbuf[p] and V(j+1) -> vbuf[1-p] (iteration j, p = j&1):
+    wave w's piece i of a tile is LDS bytes [4096w + 1024i, +1024), M0 set per
+    piece (one MFMA between the M0 write and the load: its wait state); then
+    the descriptors advance one tile"""
+    out = []
+    for i in range(4):
+        out.append(salu(f"s_add_u32 m0, %[dmab], {KBUF[p] + 1024 * i}"))
+        out.append(vmem(f"buffer_load_dwordx4 {KD(i)}, {SK}, 0 offen lds", r=[KD(i)]))
+    for i in range(4):
+        out.append(salu(f"s_add_u32 m0, %[dmab], {VBUF[1 - p] + 1024 * i}"))
+        out.append(vmem(f"buffer_load_dwordx4 {VD(i)}, {SV}, 0 offen lds", r=[VD(i)]))
+    out += [salu("s_add_u32 s40, s40, 0x4000"), salu("s_addc_u32 s41, s41, 0"),
+            salu(f"s_sub_i32 {SKREM}, {SKREM}, 0x4000"), salu(f"s_max_i32 s42, {SKREM}, 0"),
+            salu("s_add_u32 s44, s44, 0x4000"), salu("s_addc_u32 s45, s45, 0"),
+            salu(f"s_sub_i32 {SVREM}, {SVREM}, 0x4000"), salu(f"s_max_i32 s46, {SVREM}, 0")]
+    return out
+
+
+def dma_setup(st):
+    """M0 saved; per-pass DMA source offsets from the lane constants
+    (kdma = piece 0's, K(i) = (kdma + 1024 i) ^ 64 i; vdma = piece 0's, V(i) =
+    vdma + 2048 (i >> 1) + 128 (i & 1), chunk bit 1 flipped for i >= 2)"""
+    st.raw(f"s_mov_b32 {SM0}, m0")
+    st.raw(f"v_mov_b32 {KD(0)}, %[kdma]")
+    st.raw(f"v_mov_b32 {VD(0)}, %[vdma]")
+    for i in range(1, 4):
+        st.raw(f"v_add_u32 {KD(i)}, {1024 * i}, %[kdma]")
+        st.raw(f"v_xor_b32 {KD(i)}, {64 * i}, {KD(i)}")
+        st.raw(f"v_add_u32 {VD(i)}, {2048 * (i >> 1) + 128 * (i & 1)}, %[vdma]")
+        if i >= 2:
+            st.raw(f"v_xor_b32 {VD(i)}, 32, {VD(i)}")
+    st.nop(1)
+
+
+def stage_loads(st_set=0, p=None):
     """global loads of the next stage into a staging set, then the
     descriptors advance one tile (bytes left clamp at 0: no traffic past the end)"""
+    if DMA:
+        return dma_loads(p)
     out = []
     for i in range(4):
         out.append(vmem(f"buffer_load_dwordx4 {kst(i, st_set)}, {KOFF[i]}, {SK}, 0 offen", r=[KOFF[i]], w=[kst(i, st_set)]))
@@ -546,7 +609,10 @@ def phase_a(st, p, with_max, diag=False):
             put(4 * x + 1, mm[0])
             put(4 * x + 2, mm[1])
     # stage traffic: LDS writes in cb 0, loads in cb 1
-    if "nostage" not in XP and STAGE2:
+    if "nostage" not in XP and DMA:
+        for i, ld in enumerate(stage_loads(p=p)):
+            put((4 + i) if diag else (DMA_AT + i), ld)
+    elif "nostage" not in XP and STAGE2:
         for i, ld in enumerate(stage_loads(1 - p)):
             put((10 + 2 * i) if diag else (LD_AT + LD_SP * i), ld)
     if "nostage" not in XP and "stage_a" in XP and not STAGE2:
@@ -833,7 +899,12 @@ def body(st, p, causal, labels):
     st.label(L["notsteady"][p])
     st.raw(f"s_cmp_eq_u32 {SJ1}, {NTILES}")
     st.branch("s_cbranch_scc1", L["last"][p])
-    if STAGE2:
+    if DMA:
+        for ins in stage_loads(p=p):
+            st.emit(ins)
+            if isinstance(ins, Ins) and ins.text.startswith("s_add_u32 m0"):
+                st.nop(1)
+    elif STAGE2:
         for ins in stage_loads(1 - p) + stage_writes(p):
             st.emit(ins)
     else:
@@ -861,7 +932,7 @@ def body(st, p, causal, labels):
     st.raw(f"s_cmp_lt_u32 {SJ}, {SNW}")
     st.branch("s_cbranch_scc1", drain_pf)
     prefetch_next(st)
-    st.branch("s_branch", L["end"][p])
+    st.branch("s_branch", L["end_nowait" if DMA else "end"][p])
     st.label(drain_pf)
     for b in range(4):
         for cb in range(4):
@@ -875,7 +946,7 @@ def body(st, p, causal, labels):
         # prefetch's vector-memory issue
         pv_plain(st, p)
         prefetch_next(st)
-    st.branch("s_branch", L["end"][p])
+    st.branch("s_branch", L["end_nowait" if DMA else "end"][p])
     st.label(nopf)
     st.raw(f"s_cmp_lt_u32 {SJ}, {SNW}")
     st.branch("s_cbranch_scc0", L["end"][p])
@@ -885,6 +956,11 @@ def body(st, p, causal, labels):
                 st.emit(c)
     pv_plain(st, p)
     st.label(L["end"][p], drain_lgkm=True)
+    if DMA:
+        # this iteration's LDS-DMA landed before the barrier publishes it (the
+        # last iteration issues none: its next-item prefetch stays in flight)
+        st.raw("s_waitcnt vmcnt(0)")
+        st.label(L["end_nowait"][p], drain_lgkm=True)
     st.raw("s_barrier")
     stamp(st, 62)
     stamp_acc(st, 66, 62, 60)
@@ -1028,6 +1104,8 @@ def stage0(st):
     st.raw(f"s_addc_u32 s45, s45, 0")
     st.raw(f"s_sub_i32 {SVREM}, s46, 0x4000")
     st.raw(f"s_max_i32 s46, {SVREM}, 0")
+    if DMA:
+        return  # iteration 0 issues K(2), V(1) by LDS-DMA
     st.nop(4)
     for ins in stage_loads():
         st.emit(ins)
@@ -1101,11 +1179,11 @@ def prologue(st, causal, split=False):
             st.raw(f"v_mov_b32 v{x}, 0")
         for b in range(4):
             st.raw(f"v_mov_b32 {MREF[b]}, 0")
-        st.raw("s_waitcnt vmcnt(16)")
+        st.raw(f"s_waitcnt vmcnt({8 + SG0})")
     else:
         # (older than the previous item's 16 O stores)
         zero_state(st)
-        st.raw("s_waitcnt vmcnt(24)")
+        st.raw(f"s_waitcnt vmcnt({16 + SG0})")
     st.branch("s_branch", join)
     # ---- cold: the chunk's first item
     st.label(cold)
@@ -1133,7 +1211,7 @@ def prologue(st, causal, split=False):
     stage0(st)
     zero_state(st)
     # Q and K(0) landed (V(0), K(1) and stage 0 may still fly)
-    st.raw("s_waitcnt vmcnt(16)")
+    st.raw(f"s_waitcnt vmcnt({8 + SG0})")
     st.label(join)
     for i in range(4):
         st.raw(f"ds_write_b128 %[klds], {R('v', 112 + 4 * i, 4)} offset:{KBUF[0] + 4096 * i}")
@@ -1169,13 +1247,13 @@ def prologue(st, causal, split=False):
         cw, cd = newlabel("coldw"), newlabel("waitdone")
         st.raw(f"s_cmp_eq_u32 {WARM}, 0")
         st.branch("s_cbranch_scc1", cw)
-        st.raw("s_waitcnt vmcnt(24)")
+        st.raw(f"s_waitcnt vmcnt({16 + SG0})")
         st.branch("s_branch", cd)
         st.label(cw)
-        st.raw("s_waitcnt vmcnt(8)")
+        st.raw(f"s_waitcnt vmcnt({SG0})")
         st.label(cd)
     else:
-        st.raw("s_waitcnt vmcnt(8)")
+        st.raw(f"s_waitcnt vmcnt({SG0})")
     for i in range(4):
         st.raw(f"ds_write_b128 %[vlds], {vst(i, 1)} offset:{VBUF[0] + 4096 * i}")
         st.raw(f"ds_write_b128 %[klds], {kst(i, 1)} offset:{KBUF[1] + 4096 * i}")
@@ -1293,6 +1371,7 @@ def generate(causal, split=False):
     labels = {k: [newlabel(f"{k}{p}") for p in range(2)]
               for k in ("loop", "notsteady", "masked", "general", "slow", "slow2", "slow3", "end")}
     labels["last"] = [newlabel(f"last{p}") for p in range(2)]
+    labels["end_nowait"] = [newlabel(f"endnw{p}") for p in range(2)]
     labels["done"] = newlabel("done")
     item = newlabel("item")
     # the workgroup's items (a chunk of fa_w4_kernel.hpp's table) in one
@@ -1300,6 +1379,8 @@ def generate(causal, split=False):
     # last iteration
     st.raw(f"s_mov_b32 {ITEM}, 0")
     st.raw(f"s_mov_b32 {WARM}, 0")
+    if DMA:
+        dma_setup(st)
     st.label(item)
     read_item(st, causal)
     prologue(st, causal, split)
@@ -1348,6 +1429,8 @@ def generate(causal, split=False):
     st.raw(f"s_add_u32 {ITEM}, {ITEM}, 1")
     st.raw(f"s_cmp_lt_u32 {ITEM}, %[nitems]")
     st.branch("s_cbranch_scc1", item)
+    if DMA:
+        st.raw(f"s_mov_b32 m0, {SM0}")
     return st.out
 
 
@@ -1355,7 +1438,7 @@ HEADER = """// GENERATED by gen_w4_item.py -- do not edit.
 // One item (256 query rows x all key tiles) of the one-wave-per-SIMD kernel:
 // see the generator's docstring for the register map and the schedule.
 #pragma once
-"""
+""" + ("#define FA_W4_DMA 1\n" if DMA else "")
 
 
 def cxx(causal, bf16, lines, split=False):
@@ -1363,6 +1446,7 @@ def cxx(causal, bf16, lines, split=False):
     vclob = ", ".join(f'"v{i}"' for i in range(236))
     aclob = ", ".join(f'"a{i}"' for i in range(240 if STAGE2 else 208))
     sclob = ", ".join(f'"s{i}"' for i in range(40, 98))
+    dma_ops = (',\n        [kdma] "v"(ln.kdma), [vdma] "v"(ln.vdma), [dmab] "s"(rn.dmab)' if DMA else "")
     name = (("w4_item_causal" if causal else "w4_item_noncausal") + ("_split" if split else "")
             + ("_bf16" if bf16 else "_f16"))
     return f"""
@@ -1375,7 +1459,7 @@ __device__ __forceinline__ void {name}(const W4Run& rn, const W4Lane& ln) {{
         [ka0] "v"(ln.ka[0]), [ka1] "v"(ln.ka[1]), [ka2] "v"(ln.ka[2]), [ka3] "v"(ln.ka[3]),
         [va0] "v"(ln.va[0]), [va1] "v"(ln.va[1]), [koff] "v"(ln.koff), [voff] "v"(ln.voff),
         [klds] "v"(ln.klds), [vlds] "v"(ln.vlds), [vt] "v"(ln.vt), [r16] "v"(ln.r16),
-        [qoff] "v"(ln.qoff), [ooff] "v"(ln.ooff)
+        [qoff] "v"(ln.qoff), [ooff] "v"(ln.ooff){dma_ops}
       : "memory", "vcc", "scc", {sclob},
         {vclob},
         {aclob});

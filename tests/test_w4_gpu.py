@@ -152,3 +152,13 @@ def test_w4_bf16_matches_pingpong(shape, causal):
         sc = sc + torch.full((s, s), float("-inf"), device="cuda").triu(1)
     ref = torch.softmax(sc, -1) @ v.float()
     assert (out.float() - ref).abs().max().item() <= 5e-3
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("b,h,s", [(2100, 32, 64), (1100, 32, 300)])
+def test_w4_second_item_chunk(b, h, s, causal):
+    # > 256 rounds per workgroup (67,200 / 70,400 items on 256 CUs): the
+    # kernel's second item table (kW4Chunk = 256 slots per asm statement)
+    # starts cold -- ITEM/WARM reset, stale K/V images, the cross-item
+    # epilogue deferral stopped at the first chunk's last item
+    _compare(b, h, s, causal, seed=900)
