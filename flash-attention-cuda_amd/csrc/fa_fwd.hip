@@ -619,7 +619,9 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
     // the one-wave-per-SIMD asm kernel (W4, same items and order), except a
     // non-causal launch whose last round is short: the ping-pong runs that
     // tail as KV-pair halves on twice the CUs, W4 has no tail split
-    const long long per_xcd = (wg256 + 7) / 8, cus = std::min<long long>(32, per_xcd);
+    // (CUs per XCD as launch() sizes the persistent grid)
+    const long long per_xcd = (wg256 + 7) / 8,
+                    cus = std::min<long long>(std::max(1, num_cus() / 8), per_xcd);
     const long long tail = per_xcd % cus;
     if (!causal && tail > 0 && 2 * tail <= cus) return cfg_for(256, 8, 64, c, 1, 2);
     return cfg_for(256, 4, 64, c, 0, 5);

@@ -568,8 +568,9 @@ def phase_a(st, p, with_max, diag=False):
 
     n = len(mf)
     # K reads of cb 0 first; the conversions of cb 0's four blocks cover
-    # their LDS latency
-    put(0, [k_read(t, 0, t, kb) for t in range(4)])
+    # their LDS latency  (W4_XP=kpre, timing only: read in the previous phase B)
+    if "kpre" not in XP or diag or not with_max:
+        put(0, [k_read(t, 0, t, kb) for t in range(4)])
     if diag:
         # blocks above the diagonal: P(j) out of them, then -inf
         above = [(b, cb) for cb in range(4) for b in range(4) if cb > b]
@@ -657,6 +658,9 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
         put(k + 2, r[1])
     for i, ins in enumerate(leftover):
         put(1 + i, ins)
+    if "kpre" in XP and exps:  # timing only: next phase A's cb-0 K fragments (stale buffer)
+        for t in range(4):
+            put(len(mf) - 12 + 2 * t, k_read(t, 0, t, KBUF[p]))
     # stage traffic (phase A is the denser half): LDS writes of stage j, then
     # the next stage's global loads, spread over the gaps after the decision
     if "nostage" not in XP and ("stage_a" not in XP or STAGE2):

@@ -1,6 +1,8 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_w4_gpu.py -k second_item_chunk -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_chunk.log 2>&1 || { tail -30 gpurun_out/pytest_chunk.log; exit 1; }
-tail -6 gpurun_out/pytest_chunk.log
-VAR=dma bash flash-attention-cuda_amd/tools/run_var_ab.sh
+VARS=kpre OUT=r04_kpre_timing bash flash-attention-cuda_amd/tools/ab_vars.sh || exit 1
+cd flash-attention-cuda_amd
+for v in s_base s_tmajor s_bare s_kpre s_nocvt s_nomax s_nostage s_nokread s_novread; do
+  echo "== $v"
+  timeout -k 10 60 python tools/w4_stamps.py --config 38 --seq 8192 --lib $v || exit 1
+done 2>&1 | tee ../gpurun_out/r04_stamps_attr.txt

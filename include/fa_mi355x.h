@@ -146,7 +146,14 @@ int fa_fwd_bf16_ws(const void* q, const void* k, const void* v, void* o,
                    void* hip_stream);
 
 /* The dispatcher's decision (ref tier table :620-661): config id used by
- * fa_fwd_f16 for this shape. */
+ * fa_fwd_f16 for this shape.  The _ws entries may run the causal split tier
+ * instead: check fa_fwd_split_pieces() first (> 0: the split tier runs with
+ * that many 64-key tiles per piece, and this config is not used).
+ *
+ * Config ids are positions in this build's table (fa_num_configs /
+ * fa_config_info): they are not stable across releases (round 3 renumbered
+ * 0-49 to 0-43 when the table was trimmed to the dispatched tiers).  Select a
+ * tier by its fa_config_info().name, not by a remembered id. */
 int fa_select_config(int batch, int heads, int seq_len, int causal);
 
 int fa_num_configs(void);
