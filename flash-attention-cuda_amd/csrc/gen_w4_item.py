@@ -91,6 +91,9 @@ PF_BEFORE_DRAIN = os.environ.get("W4_PF_BEFORE", "0") == "1"  # V^T fragments re
 # register; its O descriptor and row base wait in s[60:63] / s64
 XOVL = os.environ.get("W4_XOVL", "1") == "1" and DIAG not in ("stamps", "pstamps")  # (s60-s69: stamps)
 ROSAVE, ROWSAVE = "s[60:63]", "s64"
+# cache policy of the (non-split) O stores; the split tier's slab stores stay
+# sc1 (read by other workgroups)
+OPOL = " ".join([""] + os.environ.get("W4_OPOL", "sc1").split("+"))  # e.g. W4_OPOL=nt, sc1+nt, ""
 
 
 def regs(spec):
@@ -624,6 +627,10 @@ def phase_a(st, p, with_max, diag=False):
         for i, ld in enumerate(stage_loads()):
             put(20 + i, ld)
     # the first V^T fragments of PV(j) (V(j) is ready since the last barrier)
+    if "vinA" in XP and with_max and not diag:  # timing only: all 16, spread over phase A
+        for f in range(16):
+            for i, r in enumerate(v_reads(f // 8, f % 8, f % 8, VBUF[p])):
+                put(6 + 3 * f + i, r)
     for f in range(V_AHEAD):
         for i, r in enumerate(v_reads(0, f, f, VBUF[p])):
             put(n - 12 - 3 * (V_AHEAD - 3) + 3 * f + i, r)
@@ -650,7 +657,7 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
         gaps.setdefault(k, []).extend(ins)
 
     # V fragments V_AHEAD ahead (the first V_AHEAD were read in phase A)
-    for f in range(V_AHEAD, 16):
+    for f in range(V_AHEAD, 16 if not ("vinA" in XP and exps and dec_gap > 0) else V_AHEAD):
         k = frag_first[f - V_AHEAD]
         u, e = divmod(f, 8)
         r = v_reads(u, e, f % 8, vb)
@@ -704,7 +711,14 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
         stamp_acc(st, 65, 60, 62)
         if DIAG == "stamps":
             st.raw("s_add_u32 s67, s67, 1")
-    st.branch("s_branch", label_end)
+    # timing only (wrong results): the steady path skips the DMA wait
+    # (novmwait) or the wait and the barrier (nobar)
+    if dec_gap > 0 and "nobar" in XP:
+        st.branch("s_branch", label_end.replace("Lend", "Lendnb"))
+    elif dec_gap > 0 and "novmwait" in XP:
+        st.branch("s_branch", label_end.replace("Lend", "Lendnw"))
+    else:
+        st.branch("s_branch", label_end)
     # slow path: the remaining PV MFMAs (no exps), then rescale
     st.label(label_slow)
     for k in range(dec_gap, len(mf)):
@@ -965,7 +979,11 @@ def body(st, p, causal, labels):
         # last iteration issues none: its next-item prefetch stays in flight)
         st.raw("s_waitcnt vmcnt(0)")
         st.label(L["end_nowait"][p], drain_lgkm=True)
+    if "novmwait" in XP and "nobar" not in XP:
+        st.label(L["end"][p].replace("Lend", "Lendnw"), drain_lgkm=True)
     st.raw("s_barrier")
+    if "nobar" in XP:
+        st.label(L["end"][p].replace("Lend", "Lendnb"), drain_lgkm=True)
     stamp(st, 62)
     stamp_acc(st, 66, 62, 60)
     st.raw(f"s_add_u32 {SJ}, {SJ}, 1")
@@ -1339,7 +1357,8 @@ def epilogue_ops(split, ro=RO, rowbase=ST1, zero_o=False):
             E(valu(f"{DT['cvt_pk']} {Y[1]}, {d[6]}, {d[7]}", r=d[6:8], w=[Y[1]]))
             for dw in range(2):
                 E(valu(f"v_permlane16_swap_b32 {X[dw]}, {Y[dw]}", r=[X[dw], Y[dw]], w=[X[dw], Y[dw]]))
-            E(vmem(f"buffer_store_dwordx4 v[152:155], {T[7]}, {ro}, 0 offen offset:{64 * ep} sc1",
+            pol = OPOL if not split else " sc1"
+            E(vmem(f"buffer_store_dwordx4 v[152:155], {T[7]}, {ro}, 0 offen offset:{64 * ep}{pol}",
                    r=["v[152:155]", T[7]]))
             E("s_nop 1")
     E("s_nop 1")
