@@ -257,8 +257,6 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(
 
 // one wave per SIMD, 64 query rows per wave, asm-owned register file
 #include "fa_w4_kernel.hpp"
-// short launches: four waves split a workgroup's flattened key tiles
-#include "fa_w4k_kernel.hpp"
 
 namespace fa {
 
@@ -342,8 +340,7 @@ struct Config {
   fa_config_info_t info;
   int sched;  // 0 = one barrier per tile, 1 = 8-wave ping-pong, 3 = ping-pong + LDS-DMA tiles
   int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent, 3 = KV-pair,
-              // 4 = KV-quad, 5 = persistent, one wave per SIMD (W4, asm item program),
-              // 6 = short tier: flattened key tiles split over the four waves (W4K)
+              // 4 = KV-quad, 5 = persistent, one wave per SIMD (W4, asm item program)
   kernel_fn fn;
 };
 
@@ -351,8 +348,7 @@ template <int W, int BN_, int C, int KIND, int SCHED, int DT, int HDIM>
 constexpr kernel_fn pick_kernel() {
   if constexpr (KIND == 5)
     return fa_fwd_f16_w4_kernel<(C != 0), DT == 1>;
-  else if constexpr (KIND == 6)
-    return fa_fwd_f16_w4k_kernel<(C != 0), DT == 1>;
+
   else if constexpr (KIND == 3)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
   else if constexpr (KIND == 4)
@@ -391,11 +387,6 @@ constexpr kernel_fn pick_kernel() {
 #define FA_CFG_W4(ID, C, DT, NAME)                                                     \
   {{ID, 256, 64, 4, C, 0, kW4LdsBytes, NAME, DT, 128}, 0, 5,                             \
    pick_kernel<4, 64, C, 5, 0, DT, 128>()}
-
-// W4K: 4 waves x 64 query rows, one or two 64-row blocks per workgroup
-#define FA_CFG_W4K(ID, C, DT, NAME)                                                    \
-  {{ID, 64, 64, 4, C, 0, kW4kLdsBytes, NAME, DT, 128}, 0, 6,                            \
-   pick_kernel<4, 64, C, 6, 0, DT, 128>()}
 
 // Only tiers the dispatcher picks, explicit entry points (split-KV) and the
 // baselines a test compares against (the per-item ping-pong 2/3: the
@@ -451,11 +442,6 @@ static const Config kConfigs[] = {
     FA_CFG_W4(41, 1, 1, "bf16_bm256_bn64_w4x64_m16_asm_persistent_causal"),
     FA_CFG(42, 4, 128, 0, 0, 0, "bm128_bn128_w4_m16_noncausal"),
     FA_CFG(43, 4, 128, 1, 0, 0, "bm128_bn128_w4_m16_causal"),
-    // short tier: 64-row blocks, the four waves split the flattened key tiles
-    FA_CFG_W4K(44, 0, 0, "bm64_bn64_w4x64_asm_keysplit_noncausal"),
-    FA_CFG_W4K(45, 1, 0, "bm64_bn64_w4x64_asm_keysplit_causal"),
-    FA_CFG_W4K(46, 0, 1, "bf16_bm64_bn64_w4x64_asm_keysplit_noncausal"),
-    FA_CFG_W4K(47, 1, 1, "bf16_bm64_bn64_w4x64_asm_keysplit_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -535,13 +521,7 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
     const long long c = std::min<long long>(std::max(1, num_cus() / 8), per_xcd);
     blocks = 8 * c;
   }
-  p.w4k_per = p.w4k_groups = 0;
-  if (cfg.kind == 6) {
-    // one 64-row block per workgroup while they fit the CUs, else two
-    p.w4k_per = blocks <= num_cus() ? 1 : 2;
-    p.w4k_groups = (int)((blocks + p.w4k_per - 1) / p.w4k_per);
-    blocks = 8 * (((long long)p.w4k_groups + 7) / 8);
-  }
+
   hipLaunchKernelGGL(cfg.fn, dim3((unsigned)blocks), dim3(cfg.info.waves * 64),
                      cfg.info.lds_bytes, stream, p);
   return hipGetLastError() == hipSuccess ? FA_OK : FA_ERR_LAUNCH;

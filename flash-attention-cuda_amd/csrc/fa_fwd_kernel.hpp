@@ -89,10 +89,6 @@ struct FwdParams {
   char* ws_o;
   int piece_tiles;
   int pmax;
-  // short tier (fa_w4k_kernel.hpp): 64-row query blocks per workgroup (1 or
-  // 2) and the number of workgroups with work
-  int w4k_per;
-  int w4k_groups;
 };
 
 // ---------------------------------------------------------------------------

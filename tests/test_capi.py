@@ -76,13 +76,6 @@ def test_config_table():
             assert c.block_m == 16 * c.waves
             assert c.lds_bytes == KVPAIR_LDS >= 4 * 17 * 64 * 16
             continue
-        if "_keysplit_" in c.name:
-            # short tier: 64-row blocks, the four waves split the key tiles;
-            # LDS = four V image pairs, the early partial, five log2-sum-exp
-            # rows and the eight segment records
-            assert c.block_m == 64 and c.waves == 4
-            assert c.lds_bytes == 4 * 2 * 64 * 256 + 64 * 256 + 5 * 256 + 8 * 128 <= 160 * 1024
-            continue
         if "_kvquad_" in c.name:
             # four waves per 32 query rows; four double-width stage buffers
             assert c.block_m == 8 * c.waves
@@ -256,7 +249,6 @@ def test_config_table_ships_only_used_tiers():
     # BN=128 (the reference's long non-causal tile, flash_attention.cu:626-634):
     # built, parity-tested and measured, not dispatched (BN=128)
     explicit |= {c.name for c in cfgs if c.block_n == 128}
-    explicit |= {c.name for c in cfgs if "_keysplit_" in c.name}  # short tier: not dispatched yet
     # head_dim 64 of the asm W4 tier runs the ping-pong persistent twins
     w4 = {n for n in used if "_asm_persistent_" in n}
     assert w4, "the W4 tier is dispatched"
