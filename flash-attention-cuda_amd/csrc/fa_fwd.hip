@@ -347,7 +347,7 @@ struct Config {
 template <int W, int BN_, int C, int KIND, int SCHED, int DT, int HDIM>
 constexpr kernel_fn pick_kernel() {
   if constexpr (KIND == 5)
-    return fa_fwd_f16_w4_kernel<(C != 0), DT == 1>;
+    return fa_fwd_f16_w4_kernel<(C != 0), DT == 1, HDIM>;
 
   else if constexpr (KIND == 3)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
@@ -384,9 +384,10 @@ constexpr kernel_fn pick_kernel() {
    pick_kernel<8, 64, C, 4, 1, DT, HDIM>()}
 
 // W4: 4 waves x 64 query rows (one wave per SIMD), K/V double-buffered (64 KB)
-#define FA_CFG_W4(ID, C, DT, NAME)                                                     \
-  {{ID, 256, 64, 4, C, 0, kW4LdsBytes, NAME, DT, 128}, 0, 5,                             \
-   pick_kernel<4, 64, C, 5, 0, DT, 128>()}
+#define FA_CFG_W4D(ID, C, DT, HDIM, NAME)                                              \
+  {{ID, 256, 64, 4, C, 0, kW4LdsBytes, NAME, DT, HDIM}, 0, 5,                            \
+   pick_kernel<4, 64, C, 5, 0, DT, HDIM>()}
+#define FA_CFG_W4(ID, C, DT, NAME) FA_CFG_W4D(ID, C, DT, 128, NAME)
 
 // Only tiers the dispatcher picks, explicit entry points (split-KV) and the
 // baselines a test compares against (the per-item ping-pong 2/3: the
@@ -442,6 +443,11 @@ static const Config kConfigs[] = {
     FA_CFG_W4(41, 1, 1, "bf16_bm256_bn64_w4x64_m16_asm_persistent_causal"),
     FA_CFG(42, 4, 128, 0, 0, 0, "bm128_bn128_w4_m16_noncausal"),
     FA_CFG(43, 4, 128, 1, 0, 0, "bm128_bn128_w4_m16_causal"),
+    // head_dim 64 twins of the W4 tier (register-staged K/V)
+    FA_CFG_W4D(44, 0, 0, 64, "d64_bm256_bn64_w4x64_m16_asm_persistent_noncausal"),
+    FA_CFG_W4D(45, 1, 0, 64, "d64_bm256_bn64_w4x64_m16_asm_persistent_causal"),
+    FA_CFG_W4D(46, 0, 1, 64, "bf16_d64_bm256_bn64_w4x64_m16_asm_persistent_noncausal"),
+    FA_CFG_W4D(47, 1, 1, 64, "bf16_d64_bm256_bn64_w4x64_m16_asm_persistent_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -650,8 +656,9 @@ static int launch_auto(int dtype, const void* q, const void* k, const void* v, v
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
   const int sel = fa_select_config(batch, heads, seq_len, causal);
   int id = twin(sel, dtype, head_dim);
-  // W4 is head_dim 128 only: head_dim 64 runs the ping-pong persistent twin
-  if (id < 0 && sel >= 0 && kConfigs[sel].kind == 5)
+  // head_dim 64 of the W4 tier: the ping-pong persistent twin until the W4
+  // head_dim-64 program is measured on the GPU
+  if (sel >= 0 && kConfigs[sel].kind == 5 && head_dim == 64)
     id = twin(cfg_for(256, 8, 64, causal ? 1 : 0, 1, 2), dtype, head_dim);
   if (id < 0) return FA_ERR_BAD_CONFIG;
   return launch(id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,

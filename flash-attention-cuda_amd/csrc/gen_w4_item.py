@@ -80,6 +80,43 @@ def set_dtype(bf16):
                             "one2": "0x3c003c00"})
     DT["bf16"] = bf16
 V_AHEAD = int(os.environ.get("W4_V_AHEAD", "3"))
+
+# head_dim of the generated function (set_hd): 128, the reference's, or 64.
+# Q/K/V/O rows are 2*hd bytes in HBM; the LDS images keep 256-B row slots at
+# either (a 64-wide row fills half a slot), as the 8-wave kernels' do
+HDC = {"hd": 128}
+
+
+def set_hd(hd):
+    HDC["hd"] = hd
+
+
+def NT():     # k-steps of a QK^T chain = Q fragments per row block
+    return HDC["hd"] // 32
+
+
+def NE():     # 16-column O^T blocks per row block
+    return HDC["hd"] // 16
+
+
+def ROWB():   # bytes of a Q/K/V/O row
+    return 2 * HDC["hd"]
+
+
+def ROWSH():
+    return 8 if HDC["hd"] == 128 else 7
+
+
+def TILEB():  # bytes of a 64-key K or V tile
+    return 64 * ROWB()
+
+
+def NPASS():  # 4-KiB register-staging passes per tile and tensor (256 lanes x 16 B)
+    return HDC["hd"] // 32
+
+
+def PASSL():  # LDS stride of a staging pass (its rows in 256-B slots)
+    return 256 * (4096 // ROWB())
 # causal diagonal tile masked block by block inside phase A (W4_DIAG_FAST=0:
 # the general mask after phase A, for A/B)
 DIAG_FAST = os.environ.get("W4_DIAG_FAST", "1") == "1"
@@ -336,7 +373,7 @@ T = [R("v", 225 + i) for i in range(11)]   # v225-v235 temporaries
 
 
 def O(b, e, i=None):
-    base = (b * 8 + e) * 4
+    base = (b * NE() + e) * 4
     return R("a", base, 4) if i is None else R("a", base + i)
 
 
@@ -345,7 +382,7 @@ def L(b, i=None):
 
 
 def Q(b, t):
-    return R("a", 144 + 16 * b + 4 * t, 4)
+    return R("a", 144 + 4 * NT() * b + 4 * t, 4)
 
 
 # LDS: K buffers at 0 / 16384, V buffers at 32768 / 49152 (lane addresses
@@ -385,7 +422,7 @@ def v_reads(u, e, slot, vb):
 def qk_chain(b, cb, slots):
     """S(b,cb) = sum_t K[t][cb] . Q[b][t]^T, C = -m_ref on the first step"""
     out = []
-    for t in range(4):
+    for t in range(NT()):
         c = NEGM(b) if t == 0 else S(b, cb)
         out.append(mfma(S(b, cb), KF(slots[t]), Q(b, t), c))
     return out
@@ -418,8 +455,8 @@ def pv_mfmas():
     """PV + row sums in M16::pv order: for u: for e: 4 b; then 4 row sums"""
     ms, frag_first = [], {}
     for u in range(2):
-        for e in range(8):
-            f = u * 8 + e
+        for e in range(NE()):
+            f = u * NE() + e
             frag_first[f] = len(ms)
             for b in range(4):
                 ms.append(mfma(O(b, e), VF(f % 8), P(b, u), O(b, e)))
@@ -448,9 +485,23 @@ DMA_AT = int(os.environ.get("W4_DMA_AT", "2"))  # first phase-A gap of the DMA s
 # registers are needed.  Issued in phase A of iteration j into the buffers
 # iteration j-1 finished reading (K(j+2) -> kbuf[j&1], V(j+1) -> vbuf[(j+1)&1])
 # and waited for (vmcnt(0)) before the iteration's barrier.
-DMA = "regstage" not in XP
+DMA_ON = "regstage" not in XP
 SM0 = "s70"          # M0 of the enclosing code, restored at the end
-SG0 = 0 if DMA else 8  # prologue stage-0 loads in flight (none under DMA)
+
+
+def dma():
+    """LDS-DMA staging (head_dim 128); head_dim 64 stages through registers:
+    its rows fill half of an image's 256-B slots, so a lane-linear DMA piece
+    would move half padding"""
+    return DMA_ON and HDC["hd"] == 128
+
+
+def sg0():  # prologue stage-0 loads in flight (none under DMA)
+    return 0 if dma() else 2 * NPASS()
+
+
+def nst():  # an item's O stores per wave
+    return 2 * NE()
 
 
 def KD(i):
@@ -472,13 +523,13 @@ def vst(i, st_set):
 def stage_writes(p):
     """LDS writes of stage j (K(j+2) -> kbuf[j&1], V(j+1) -> vbuf[(j+1)&1]);
     with two sets the 8 youngest loads (stage j+1) may still be in flight"""
-    if DMA:
+    if dma():
         return []
     ss = p if STAGE2 else 0
-    out = [f"s_waitcnt vmcnt({8 if STAGE2 else 0})"]
-    for i in range(4):
-        out.append(dsw(f"ds_write_b128 %[klds], {kst(i, ss)} offset:{KBUF[p] + 4096 * i}", "%[klds]", kst(i, ss)))
-        out.append(dsw(f"ds_write_b128 %[vlds], {vst(i, ss)} offset:{VBUF[1 - p] + 4096 * i}", "%[vlds]", vst(i, ss)))
+    out = [f"s_waitcnt vmcnt({2 * NPASS() if STAGE2 else 0})"]
+    for i in range(NPASS()):
+        out.append(dsw(f"ds_write_b128 %[klds], {kst(i, ss)} offset:{KBUF[p] + PASSL() * i}", "%[klds]", kst(i, ss)))
+        out.append(dsw(f"ds_write_b128 %[vlds], {vst(i, ss)} offset:{VBUF[1 - p] + PASSL() * i}", "%[vlds]", vst(i, ss)))
     return out
 
 
@@ -520,24 +571,29 @@ def dma_setup(st):
 def stage_loads(st_set=0, p=None):
     """global loads of the next stage into a staging set, then the
     descriptors advance one tile (bytes left clamp at 0: no traffic past the end)"""
-    if DMA:
+    if dma():
         return dma_loads(p)
     out = []
-    for i in range(4):
+    for i in range(NPASS()):
         out.append(vmem(f"buffer_load_dwordx4 {kst(i, st_set)}, {KOFF[i]}, {SK}, 0 offen", r=[KOFF[i]], w=[kst(i, st_set)]))
         out.append(vmem(f"buffer_load_dwordx4 {vst(i, st_set)}, {VOFF[i]}, {SV}, 0 offen", r=[VOFF[i]], w=[vst(i, st_set)]))
     if "noadv" in XP:  # timing only: every stage re-reads the same (L1-hot) tile
         return out + [salu("s_nop 0")] * 8
-    out += [salu("s_add_u32 s40, s40, 0x4000"), salu("s_addc_u32 s41, s41, 0"),
-            salu(f"s_sub_i32 {SKREM}, {SKREM}, 0x4000"), salu(f"s_max_i32 s42, {SKREM}, 0"),
-            salu("s_add_u32 s44, s44, 0x4000"), salu("s_addc_u32 s45, s45, 0"),
-            salu(f"s_sub_i32 {SVREM}, {SVREM}, 0x4000"), salu(f"s_max_i32 s46, {SVREM}, 0")]
+    tb = hex(TILEB())
+    out += [salu(f"s_add_u32 s40, s40, {tb}"), salu("s_addc_u32 s41, s41, 0"),
+            salu(f"s_sub_i32 {SKREM}, {SKREM}, {tb}"), salu(f"s_max_i32 s42, {SKREM}, 0"),
+            salu(f"s_add_u32 s44, s44, {tb}"), salu("s_addc_u32 s45, s45, 0"),
+            salu(f"s_sub_i32 {SVREM}, {SVREM}, {tb}"), salu(f"s_max_i32 s46, {SVREM}, 0")]
     return out
 
 
 # ---------------------------------------------------------------------------
 # program pieces
 # ---------------------------------------------------------------------------
+def lag():
+    return 2 if NT() == 4 else 3
+
+
 def phase_a(st, p, with_max, diag=False):
     """QK^T(j+1) from kbuf[(j+1)&1] beside cvt P(j), maxima of S(j+1), staging.
     diag: the wave's causal diagonal tile with its keys aligned to its rows
@@ -557,7 +613,7 @@ def phase_a(st, p, with_max, diag=False):
                 mf += [ch[b][t] for b in range(4)]
     else:
         for x, (b, cb) in enumerate(chains):
-            slots = [4 * (cb & 1) + t for t in range(4)]
+            slots = [4 * (cb & 1) + t for t in range(NT())]
             mf += qk_chain(b, cb, slots)
     gaps = {}
 
@@ -573,14 +629,14 @@ def phase_a(st, p, with_max, diag=False):
     # K reads of cb 0 first; the conversions of cb 0's four blocks cover
     # their LDS latency  (W4_XP=kpre, timing only: read in the previous phase B)
     if "kpre" not in XP or diag or not with_max:
-        put(0, [k_read(t, 0, t, kb) for t in range(4)])
+        put(0, [k_read(t, 0, t, kb) for t in range(NT())])
     if diag:
         # blocks above the diagonal: P(j) out of them, then -inf
         above = [(b, cb) for cb in range(4) for b in range(4) if cb > b]
         for k, (b, cb) in enumerate(above):
             ins = cvt_block(b, cb)
             ins += [valu(f"v_mov_b32 {S(b, cb, i)}, {VNINF}", r=[VNINF], w=[S(b, cb, i)]) for i in range(4)]
-            put(5 + 5 * k, ins)
+            put((5 + 5 * k) if NT() == 4 else (2 + 3 * k), ins)
     for x, (b, cb) in enumerate(chains):
         c = cvt_block(b, cb)
         if "nocvt" in XP:
@@ -591,34 +647,39 @@ def phase_a(st, p, with_max, diag=False):
             put(4 * x - 2, c[0])
             put(4 * x - 1, c[1])
         else:
-            put(4 * x - 1, c[0])
-            put(4 * x, c[1])
+            put(NT() * x - 1, c[0])
+            put(NT() * x, c[1])
         if diag and b == cb:
             # the diagonal block: key 16cb + 4sg + i is valid iff i <= r16 - 4sg
             for i in range(4):
                 xr = S(b, cb, i)
-                put(min(4 * x + 8, n), [valu(f"v_cmp_le_i32 vcc, {i}, %[vt]", r=["%[vt]"]),
+                put(min(NT() * x + 2 * NT(), n), [valu(f"v_cmp_le_i32 vcc, {i}, %[vt]", r=["%[vt]"]),
                                 valu(f"v_cndmask_b32 {xr}, {VNINF}, {xr}, vcc", r=[VNINF, xr], w=[xr])])
         # next cb's K fragments early in this cb's first chain (kspread: one
         # per chain of this cb)
         if "kspread" in XP and cb < 3 and not diag:
             put(4 * x + 1, k_read(b, cb + 1, 4 * ((cb + 1) & 1) + b, kb))
         elif b == (cb if diag else 0) and cb < 3:
-            for t in range(4):
-                put(4 * x + 1 + t % 3, k_read(t, cb + 1, 4 * ((cb + 1) & 1) + t, kb))
-        if with_max and x >= 2 and "nomax" not in XP:
-            y = x - 2
+            for t in range(NT()):
+                put(NT() * x + 1 + t % 3, k_read(t, cb + 1, 4 * ((cb + 1) & 1) + t, kb))
+        # the running maxima of chain x - LAG (its MFMA results clear of the
+        # 12-wait-state MFMA -> VALU window)
+        if with_max and x >= lag() and "nomax" not in XP:
+            y = x - lag()
             by, cby = chains[y]
             mm = max_block(by, cby, first=(cby == 0 and by in (0, 2)))
-            put(4 * x + 1, mm[0])
-            put(4 * x + 2, mm[1])
+            put(NT() * x + 1, mm[0])
+            put(NT() * x + 2, mm[1])
     # stage traffic: LDS writes in cb 0, loads in cb 1
-    if "nostage" not in XP and DMA:
+    if "nostage" not in XP and dma():
         for i, ld in enumerate(stage_loads(p=p)):
             put((4 + i) if diag else (DMA_AT + i), ld)
     elif "nostage" not in XP and STAGE2:
         for i, ld in enumerate(stage_loads(1 - p)):
-            put((10 + 2 * i) if diag else (LD_AT + LD_SP * i), ld)
+            if HDC["hd"] == 128:
+                put((10 + 2 * i) if diag else (LD_AT + LD_SP * i), ld)
+            else:
+                put((2 + i) if diag else (4 + 2 * i), ld)
     if "nostage" not in XP and "stage_a" in XP and not STAGE2:
         sw = stage_writes(p)
         put(0, sw[:1])
@@ -638,7 +699,7 @@ def phase_a(st, p, with_max, diag=False):
     st.interleave(mf, gaps)
     leftover = []
     if with_max and "nomax" not in XP:
-        for y in (len(chains) - 2, len(chains) - 1):
+        for y in range(len(chains) - lag(), len(chains)):
             by, cby = chains[y]
             leftover += max_block(by, cby, first=False)
     return leftover
@@ -657,9 +718,9 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
         gaps.setdefault(k, []).extend(ins)
 
     # V fragments V_AHEAD ahead (the first V_AHEAD were read in phase A)
-    for f in range(V_AHEAD, 16 if not ("vinA" in XP and exps and dec_gap > 0) else V_AHEAD):
+    for f in range(V_AHEAD, 2 * NE() if not ("vinA" in XP and exps and dec_gap > 0) else V_AHEAD):
         k = frag_first[f - V_AHEAD]
-        u, e = divmod(f, 8)
+        u, e = divmod(f, NE())
         r = v_reads(u, e, f % 8, vb)
         put(k + 1, r[0])
         put(k + 2, r[1])
@@ -753,7 +814,7 @@ def shift_block(st, b, sh, first):
     if not first:
         alpha = T[3]
         st.emit(valu(f"v_exp_f32 {alpha}, -{sh}", r=[sh], w=[alpha], kind="trans"))
-        for e in range(8):
+        for e in range(NE()):
             for i in range(4):
                 a = O(b, e, i)
                 st.emit(valu(f"v_accvgpr_read_b32 {T[4]}, {a}", r=[a], w=[T[4]]))
@@ -855,10 +916,10 @@ def full_max(st):
 def qk_plain(st, kb):
     """QK^T of one tile, not interleaved (prologue)"""
     for cb in range(4):
-        for t in range(4):
+        for t in range(NT()):
             st.emit(k_read(t, cb, 4 * (cb & 1) + t, kb))
         for b in range(4):
-            for m in qk_chain(b, cb, [4 * (cb & 1) + t for t in range(4)]):
+            for m in qk_chain(b, cb, [4 * (cb & 1) + t for t in range(NT())]):
                 st.emit(m)
 
 
@@ -866,8 +927,8 @@ def pv_plain(st, p):
     vb = VBUF[p]
     mf, frag_first = pv_mfmas()
     gaps = {}
-    for f in range(16):
-        u, e = divmod(f, 8)
+    for f in range(2 * NE()):
+        u, e = divmod(f, NE())
         k = frag_first[f - 2] + 1 if f >= 2 else 0
         for i, r in enumerate(v_reads(u, e, f % 8, vb)):
             gaps.setdefault(k + i if f >= 2 else 0, []).append(r)
@@ -917,7 +978,7 @@ def body(st, p, causal, labels):
     st.label(L["notsteady"][p])
     st.raw(f"s_cmp_eq_u32 {SJ1}, {NTILES}")
     st.branch("s_cbranch_scc1", L["last"][p])
-    if DMA:
+    if dma():
         for ins in stage_loads(p=p):
             st.emit(ins)
             if isinstance(ins, Ins) and ins.text.startswith("s_add_u32 m0"):
@@ -950,7 +1011,7 @@ def body(st, p, causal, labels):
     st.raw(f"s_cmp_lt_u32 {SJ}, {SNW}")
     st.branch("s_cbranch_scc1", drain_pf)
     prefetch_next(st)
-    st.branch("s_branch", L["end_nowait" if DMA else "end"][p])
+    st.branch("s_branch", L["end_nowait" if dma() else "end"][p])
     st.label(drain_pf)
     for b in range(4):
         for cb in range(4):
@@ -964,7 +1025,7 @@ def body(st, p, causal, labels):
         # prefetch's vector-memory issue
         pv_plain(st, p)
         prefetch_next(st)
-    st.branch("s_branch", L["end_nowait" if DMA else "end"][p])
+    st.branch("s_branch", L["end_nowait" if dma() else "end"][p])
     st.label(nopf)
     st.raw(f"s_cmp_lt_u32 {SJ}, {SNW}")
     st.branch("s_cbranch_scc0", L["end"][p])
@@ -974,7 +1035,7 @@ def body(st, p, causal, labels):
                 st.emit(c)
     pv_plain(st, p)
     st.label(L["end"][p], drain_lgkm=True)
-    if DMA:
+    if dma():
         # this iteration's LDS-DMA landed before the barrier publishes it (the
         # last iteration issues none: its next-item prefetch stays in flight)
         st.raw("s_waitcnt vmcnt(0)")
@@ -992,6 +1053,22 @@ def body(st, p, causal, labels):
         st.branch("s_cbranch_scc0", L["done"])
     else:
         st.branch("s_cbranch_scc1", L["loop"][0])
+
+
+def prostamp(st, i):
+    """diagnostic (W4_DIAG=prostamps): per-wave accumulated cycles of the
+    prologue's phases, in the DMA-freed v184-v207 (lanes identical):
+    v197 = last stamp, v200 + i += cycles since it; v206 = items"""
+    if DIAG != "prostamps":
+        return
+    st.raw("s_memtime s[58:59]")
+    st.raw("s_waitcnt lgkmcnt(0)")
+    st.lgkm = []
+    st.raw("v_mov_b32 v198, s58")
+    if i >= 0:
+        st.raw("v_sub_u32 v196, v198, v197")
+        st.raw(f"v_add_u32 v{200 + i}, v{200 + i}, v196")
+    st.raw("v_mov_b32 v197, v198")
 
 
 def pstamp(st, dst):
@@ -1087,7 +1164,7 @@ def prefetch_next(st):
     rsrc(st, 84, ST0, ST1, "%[qrec]")
     st.raw(f"v_readfirstlane_b32 {ST0}, v121")            # next q0
     st.raw(f"s_add_u32 {ST0}, {ST0}, %[woff]")
-    st.raw(f"s_lshl_b32 {ST0}, {ST0}, 8")
+    st.raw(f"s_lshl_b32 {ST0}, {ST0}, {ROWSH()}")
     st.raw(f"v_readfirstlane_b32 s57, v120")              # next K/V bytes
     st.raw(f"v_readfirstlane_b32 s94, v114")               # next K base
     st.raw(f"v_readfirstlane_b32 s95, v115")
@@ -1096,37 +1173,38 @@ def prefetch_next(st):
     for b in range(4):
         st.raw(f"v_add_u32 {T[b]}, {ST0}, %[qoff]")
         if b:
-            st.raw(f"v_add_u32 {T[b]}, {4096 * b}, {T[b]}")
+            st.raw(f"v_add_u32 {T[b]}, {16 * ROWB() * b}, {T[b]}")
     st.nop(4)
     for b in range(4):
-        for t in range(4):
-            st.raw(f"buffer_load_dwordx4 {R('v', 16 * b + 4 * t, 4)}, {T[b]}, {NX}, 0 offen offset:{64 * t}")
+        for t in range(NT()):
+            st.raw(f"buffer_load_dwordx4 {R('v', 4 * NT() * b + 4 * t, 4)}, {T[b]}, {NX}, 0 offen offset:{64 * t}")
     rsrc(st, 84, "s94", "s95", "s57")
     st.nop(4)
-    for i in range(4):
+    for i in range(NPASS()):
         st.raw(f"buffer_load_dwordx4 {R('v', 112 + 4 * i, 4)}, {KOFF[i]}, {NX}, 0 offen")
-    for i in range(4):
-        st.raw(f"v_add_u32 {T[4 + i]}, 0x4000, {KOFF[i]}")
+    for i in range(NPASS()):
+        st.raw(f"v_add_u32 {T[4 + i]}, {hex(TILEB())}, {KOFF[i]}")
     st.nop(1)
-    for i in range(4):
+    for i in range(NPASS()):
         st.raw(f"buffer_load_dwordx4 {kst(i, 1)}, {T[4 + i]}, {NX}, 0 offen")
     rsrc(st, 84, "s96", "s97", "s57")
     st.nop(4)
-    for i in range(4):
+    for i in range(NPASS()):
         st.raw(f"buffer_load_dwordx4 {vst(i, 1)}, {VOFF[i]}, {NX}, 0 offen")
 
 
 def stage0(st):
     """staging descriptors start at tiles K(2) / V(1); stage 0's loads"""
-    st.raw(f"s_add_u32 s40, s40, 0x8000")
+    t2, t1 = hex(2 * TILEB()), hex(TILEB())
+    st.raw(f"s_add_u32 s40, s40, {t2}")
     st.raw(f"s_addc_u32 s41, s41, 0")
-    st.raw(f"s_sub_i32 {SKREM}, s42, 0x8000")
+    st.raw(f"s_sub_i32 {SKREM}, s42, {t2}")
     st.raw(f"s_max_i32 s42, {SKREM}, 0")
-    st.raw(f"s_add_u32 s44, s44, 0x4000")
+    st.raw(f"s_add_u32 s44, s44, {t1}")
     st.raw(f"s_addc_u32 s45, s45, 0")
-    st.raw(f"s_sub_i32 {SVREM}, s46, 0x4000")
+    st.raw(f"s_sub_i32 {SVREM}, s46, {t1}")
     st.raw(f"s_max_i32 s46, {SVREM}, 0")
-    if DMA:
+    if dma():
         return  # iteration 0 issues K(2), V(1) by LDS-DMA
     st.nop(4)
     for ins in stage_loads():
@@ -1135,7 +1213,7 @@ def stage0(st):
 
 def zero_state(st):
     """O, l, -m_ref, m_ref = 0"""
-    for x in range(144):
+    for x in list(range(16 * NE())) + list(range(128, 144)):
         st.raw(f"v_accvgpr_write_b32 a{x}, 0")
     for x in range(96, 112):
         st.raw(f"v_mov_b32 v{x}, 0")
@@ -1146,7 +1224,7 @@ def zero_state(st):
 def q_scale(st):
     """Q * c (fp32 product, rounded to fp16 once: M16::scale_q) from v0-63
     into AGPRs, eight elements at a time in the (free) V^T fragment registers"""
-    for x0 in range(0, 64, 8):
+    for x0 in range(0, 16 * NT(), 8):
         xs = range(x0, x0 + 8)
         lo = {x: f"v{144 + 3 * (x - x0)}" for x in xs}
         hi = {x: f"v{145 + 3 * (x - x0)}" for x in xs}
@@ -1201,43 +1279,45 @@ def prologue(st, causal, split=False):
             st.raw(f"v_mov_b32 v{x}, 0")
         for b in range(4):
             st.raw(f"v_mov_b32 {MREF[b]}, 0")
-        st.raw(f"s_waitcnt vmcnt({8 + SG0})")
+        st.raw(f"s_waitcnt vmcnt({2 * NPASS() + sg0()})")
     else:
-        # (older than the previous item's 16 O stores)
+        # (older than the previous item's O stores)
         zero_state(st)
-        st.raw(f"s_waitcnt vmcnt({16 + SG0})")
+        st.raw(f"s_waitcnt vmcnt({nst() + sg0()})")
+    prostamp(st, 0)  # item start -> Q, K(0) landed (warm items)
     st.branch("s_branch", join)
     # ---- cold: the chunk's first item
     st.label(cold)
     # Q rows qw + 16b + r16: offset (qw + 16b) * 256 + %[qoff]
-    st.raw(f"s_lshl_b32 {ST0}, {QW}, 8")
+    st.raw(f"s_lshl_b32 {ST0}, {QW}, {ROWSH()}")
     for b in range(4):
         st.raw(f"v_add_u32 {T[b]}, {ST0}, %[qoff]")
         if b:
-            st.raw(f"v_add_u32 {T[b]}, {4096 * b}, {T[b]}")
+            st.raw(f"v_add_u32 {T[b]}, {16 * ROWB() * b}, {T[b]}")
     st.nop(1)
     for b in range(4):
-        for t in range(4):
-            st.raw(f"buffer_load_dwordx4 {R('v', 16 * b + 4 * t, 4)}, {T[b]}, {RQ}, 0 offen offset:{64 * t}")
+        for t in range(NT()):
+            st.raw(f"buffer_load_dwordx4 {R('v', 4 * NT() * b + 4 * t, 4)}, {T[b]}, {RQ}, 0 offen offset:{64 * t}")
     # K(0) -> v112.., then V(0) and K(1) into staging set 1 (a224.., a208..:
     # free until iteration 0's loads), waited for only after S(0)
-    for i in range(4):
+    for i in range(NPASS()):
         st.raw(f"buffer_load_dwordx4 {R('v', 112 + 4 * i, 4)}, {KOFF[i]}, {SK}, 0 offen")
-    for i in range(4):
+    for i in range(NPASS()):
         st.raw(f"buffer_load_dwordx4 {vst(i, 1)}, {VOFF[i]}, {SV}, 0 offen")
-    for i in range(4):
-        st.raw(f"v_add_u32 {T[4 + i]}, 0x4000, {KOFF[i]}")
+    for i in range(NPASS()):
+        st.raw(f"v_add_u32 {T[4 + i]}, {hex(TILEB())}, {KOFF[i]}")
     st.nop(1)
-    for i in range(4):
+    for i in range(NPASS()):
         st.raw(f"buffer_load_dwordx4 {kst(i, 1)}, {T[4 + i]}, {SK}, 0 offen")
     stage0(st)
     zero_state(st)
     # Q and K(0) landed (V(0), K(1) and stage 0 may still fly)
-    st.raw(f"s_waitcnt vmcnt({8 + SG0})")
+    st.raw(f"s_waitcnt vmcnt({2 * NPASS() + sg0()})")
     st.label(join)
-    for i in range(4):
-        st.raw(f"ds_write_b128 %[klds], {R('v', 112 + 4 * i, 4)} offset:{KBUF[0] + 4096 * i}")
+    for i in range(NPASS()):
+        st.raw(f"ds_write_b128 %[klds], {R('v', 112 + 4 * i, 4)} offset:{KBUF[0] + PASSL() * i}")
     q_scale(st)
+    prostamp(st, 1)  # -> K(0) written, Q scaled
     st.raw("s_waitcnt lgkmcnt(0)")
     st.raw("s_barrier")
     st.nop(2)
@@ -1253,6 +1333,7 @@ def prologue(st, causal, split=False):
         st.label(s0done)
     else:
         qk_plain(st, KBUF[0])
+    prostamp(st, 2)  # -> S(0) (+ the deferred epilogue) done
     st.raw(f"s_cmp_eq_u32 {SMASKJ}, 1")
     skip = newlabel("nomask0")
     st.branch("s_cbranch_scc0", skip)
@@ -1263,25 +1344,27 @@ def prologue(st, causal, split=False):
     slow_softmax(st, first=True)
     for e in exp_ops():
         st.emit(e)
+    prostamp(st, 3)  # -> first softmax + exp2 done
     # V(0), K(1) landed: into their LDS images (warm with the deferred
     # epilogue: its 16 O stores are the youngest, behind stage 0's 8 loads)
     if xovl:
         cw, cd = newlabel("coldw"), newlabel("waitdone")
         st.raw(f"s_cmp_eq_u32 {WARM}, 0")
         st.branch("s_cbranch_scc1", cw)
-        st.raw(f"s_waitcnt vmcnt({16 + SG0})")
+        st.raw(f"s_waitcnt vmcnt({nst() + sg0()})")
         st.branch("s_branch", cd)
         st.label(cw)
-        st.raw(f"s_waitcnt vmcnt({SG0})")
+        st.raw(f"s_waitcnt vmcnt({sg0()})")
         st.label(cd)
     else:
-        st.raw(f"s_waitcnt vmcnt({SG0})")
-    for i in range(4):
-        st.raw(f"ds_write_b128 %[vlds], {vst(i, 1)} offset:{VBUF[0] + 4096 * i}")
-        st.raw(f"ds_write_b128 %[klds], {kst(i, 1)} offset:{KBUF[1] + 4096 * i}")
+        st.raw(f"s_waitcnt vmcnt({sg0()})")
+    for i in range(NPASS()):
+        st.raw(f"ds_write_b128 %[vlds], {vst(i, 1)} offset:{VBUF[0] + PASSL() * i}")
+        st.raw(f"ds_write_b128 %[klds], {kst(i, 1)} offset:{KBUF[1] + PASSL() * i}")
     st.raw("s_waitcnt lgkmcnt(0)")
     st.lgkm = []
     st.raw("s_barrier")
+    prostamp(st, 4)  # -> V(0), K(1) written, loop start
     pstamp(st, 62)
     st.raw(f"s_mov_b32 {SJ}, 0")
     if DIAG == "stamps":
@@ -1335,8 +1418,8 @@ def epilogue_ops(split, ro=RO, rowbase=ST1, zero_o=False):
         # row offset: (qw + 16b + r16) * 256 + 2 * dlane
         E(valu(f"v_add_u32 {T[7]}, {rowbase}, %[ooff]", r=["%[ooff]"], w=[T[7]]))
         if b:
-            E(valu(f"v_add_u32 {T[7]}, {4096 * b}, {T[7]}", r=[T[7]], w=[T[7]]))
-        for ep in range(4):
+            E(valu(f"v_add_u32 {T[7]}, {16 * ROWB() * b}, {T[7]}", r=[T[7]], w=[T[7]]))
+        for ep in range(NE() // 2):
             d = [f"v{144 + i}" for i in range(8)]  # O staging: the (free) V^T fragment slots
             for x in range(2):
                 e = 2 * ep + x
@@ -1377,11 +1460,11 @@ def s0_with_epilogue(st):
     mf, gaps = [], {}
     for cb in range(4):
         for b in range(4):
-            mf += qk_chain(b, cb, [4 * (cb & 1) + t for t in range(4)])
-    gaps[0] = [k_read(t, 0, t, kb) for t in range(4)]
+            mf += qk_chain(b, cb, [4 * (cb & 1) + t for t in range(NT())])
+    gaps[0] = [k_read(t, 0, t, kb) for t in range(NT())]
     for cb in range(3):
-        for t in range(4):
-            gaps.setdefault(16 * cb + 1 + t, []).append(k_read(t, cb + 1, 4 * ((cb + 1) & 1) + t, kb))
+        for t in range(NT()):
+            gaps.setdefault(4 * NT() * cb + 1 + t, []).append(k_read(t, cb + 1, 4 * ((cb + 1) & 1) + t, kb))
     ops = epilogue_ops(False, ro=ROSAVE, rowbase=ROWSAVE, zero_o=True)
     n = len(mf)
     for i, op in enumerate(ops):
@@ -1402,14 +1485,21 @@ def generate(causal, split=False):
     # last iteration
     st.raw(f"s_mov_b32 {ITEM}, 0")
     st.raw(f"s_mov_b32 {WARM}, 0")
-    if DMA:
+    if dma():
         dma_setup(st)
+    if DIAG == "prostamps":
+        for r in range(200, 208):
+            st.raw(f"v_mov_b32 v{r}, 0")
     st.label(item)
+    prostamp(st, -1)
+    if DIAG == "prostamps":
+        st.raw("v_add_u32 v206, 1, v206")
     read_item(st, causal)
     prologue(st, causal, split)
     body(st, 0, causal, labels)
     body(st, 1, causal, labels)
     st.label(labels["done"], drain_lgkm=True)
+    prostamp(st, 5)  # loop (every iteration incl. the last one's prefetch)
     pstamp(st, 64)
     if XOVL and not split:
         # a successor follows: defer this item's epilogue into its prologue
@@ -1419,12 +1509,12 @@ def generate(causal, split=False):
         st.branch("s_cbranch_scc0", last)
         for i in range(4):
             st.raw(f"s_mov_b32 s{60 + i}, s{76 + i}")
-        st.raw(f"s_lshl_b32 {ROWSAVE}, {QW}, 8")
+        st.raw(f"s_lshl_b32 {ROWSAVE}, {QW}, {ROWSH()}")
         st.raw(f"s_mov_b32 {ITEM}, {ST0}")
         st.raw(f"s_branch {item}")
         st.label(last)
-    # ST1 = qw * 256: the epilogue's row base
-    st.raw(f"s_lshl_b32 {ST1}, {QW}, 8")
+    # ST1 = qw * row bytes: the epilogue's row base
+    st.raw(f"s_lshl_b32 {ST1}, {QW}, {ROWSH()}")
     st.nop(1)
     epilogue(st, split)
     if DIAG == "pstamps":
@@ -1440,6 +1530,16 @@ def generate(causal, split=False):
         st.nop(2)
         st.raw(f"buffer_store_dwordx4 v[120:123], v124, {RO}, 0 offen")
         st.nop(2)
+    if DIAG == "prostamps":
+        # the wave's sums over its items: [Q wait, q_scale, S(0) + deferred
+        # epilogue, first softmax, V(0)/K(1) writes, loop] + items, in
+        # O[qw][0:16] of the chunk's last item
+        st.raw("s_waitcnt vmcnt(0)")
+        st.raw(f"v_mov_b32 v199, s{ST1[1:]}")
+        st.nop(2)
+        st.raw(f"buffer_store_dwordx4 v[200:203], v199, {RO}, 0 offen")
+        st.raw(f"buffer_store_dwordx4 v[204:207], v199, {RO}, 0 offen offset:16")
+        st.nop(2)
     if DIAG == "stamps":
         # [phase A, phase B, barrier (wait + skew), steady iterations] of
         # this wave, in O[qw][0:8] (every lane the same 16 bytes)
@@ -1452,7 +1552,7 @@ def generate(causal, split=False):
     st.raw(f"s_add_u32 {ITEM}, {ITEM}, 1")
     st.raw(f"s_cmp_lt_u32 {ITEM}, %[nitems]")
     st.branch("s_cbranch_scc1", item)
-    if DMA:
+    if dma():
         st.raw(f"s_mov_b32 m0, {SM0}")
     return st.out
 
@@ -1461,7 +1561,7 @@ HEADER = """// GENERATED by gen_w4_item.py -- do not edit.
 // One item (256 query rows x all key tiles) of the one-wave-per-SIMD kernel:
 // see the generator's docstring for the register map and the schedule.
 #pragma once
-""" + ("#define FA_W4_DMA 1\n" if DMA else "")
+"""
 
 
 def cxx(causal, bf16, lines, split=False):
@@ -1469,9 +1569,9 @@ def cxx(causal, bf16, lines, split=False):
     vclob = ", ".join(f'"v{i}"' for i in range(236))
     aclob = ", ".join(f'"a{i}"' for i in range(240 if STAGE2 else 208))
     sclob = ", ".join(f'"s{i}"' for i in range(40, 98))
-    dma_ops = (',\n        [kdma] "v"(ln.kdma), [vdma] "v"(ln.vdma), [dmab] "s"(rn.dmab)' if DMA else "")
+    dma_ops = (',\n        [kdma] "v"(ln.kdma), [vdma] "v"(ln.vdma), [dmab] "s"(rn.dmab)' if dma() else "")
     name = (("w4_item_causal" if causal else "w4_item_noncausal") + ("_split" if split else "")
-            + ("_bf16" if bf16 else "_f16"))
+            + ("_d64" if HDC["hd"] == 64 else "") + ("_bf16" if bf16 else "_f16"))
     return f"""
 __device__ __forceinline__ void {name}(const W4Run& rn, const W4Lane& ln) {{
   asm volatile(
@@ -1501,6 +1601,14 @@ def main():
         # one key piece of a causal query block (fa_w4_kernel.hpp: split tier)
         _lbl[0] = 0
         text += cxx(True, bf16, generate(True, split=True), split=True)
+    # head_dim 64 (non-split)
+    set_hd(64)
+    for bf16 in (False, True):
+        set_dtype(bf16)
+        for causal in (False, True):
+            _lbl[0] = 0
+            text += cxx(causal, bf16, generate(causal))
+    set_hd(128)
     with open(out, "w") as f:
         f.write(text)
 

@@ -21,9 +21,9 @@ Derived per launch (first launch of each shape dropped):
   tflops_prof = algorithmic FLOPs / profiled kernel time (the SAME dispatches
                 the counters come from; profiled runs hold a lower clock, so
                 this is below the un-profiled HIP-event TFLOP/s)
-  identity    = mfma_busy x eff_clock x 1024 SIMDs x 1024 FLOP/clk
-                / (MFMA FLOPs issued per useful FLOP) / tflops_prof -- 1.00
-                when busy cycles, clock and time all come from one run
+  ghz_in_kernel = s_memtime cycles / s_memrealtime time per workgroup, median,
+                from the stamps build after >= 2 s of launches (tier_pmc.py
+                clocks); eff_clock is left out below 0.3 ms, where it reads high
   frac_nominal = TFLOP/s (un-profiled, HIP events) / 2516.6
   hbm_gbs     = (FETCH + WRITE bytes) / un-profiled time
 """
@@ -110,6 +110,57 @@ def run(time_it):
         del q, k, v, o
 
 
+def clocks():
+    """In-kernel clock per shape from the stamps build (lib/libfa_mi355x_stamps.so,
+    `make stamps`: every workgroup records s_memtime cycles and s_memrealtime
+    ticks over its lifetime): GHz = cycles / (ticks x 10 ns), median over the
+    launch's workgroups, after >= 2 s of back-to-back launches of the shape
+    (MI355X_MICROARCH.md DVFS note 6).  Valid on short dispatches too, where
+    GRBM_GUI_ACTIVE / kernel time reads high.  Tiers without stamps (the
+    split tier) print no clock."""
+    import ctypes
+    import time
+
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, here)
+    import torch
+    import fa_mi355x as fa
+
+    fa.LIB_PATH = os.path.join(here, "lib", "libfa_mi355x_stamps.so")
+    lib = fa.load_library()
+    lib.fa_debug_timeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    names = {c.name: c.id for c in fa.configs()}
+    n = 4096
+    buf = (ctypes.c_ulonglong * (4 * n))()
+    for label, b, h, s, causal, *forced in SHAPES:
+        shape = (b, h, s, 128)
+        q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5, generator=g)
+                   for _ in range(3))
+        o = torch.empty_like(q)
+        cfg = (None if forced[0] == "auto" else names[forced[0]]) if forced else fa.select_config(b, h, s, causal)
+        ctypes.memset(buf, 0, ctypes.sizeof(buf))
+        lib.fa_debug_timeline(buf, n)  # (clears nothing on the device: records are per launch)
+        t0 = time.time()
+        while time.time() - t0 < 2.0:
+            for _ in range(5):
+                fa.flash_attention_fwd(q, k, v, causal, out=o, config=cfg)
+            torch.cuda.synchronize()
+        fa.flash_attention_fwd(q, k, v, causal, out=o, config=cfg)
+        torch.cuda.synchronize()
+        ctypes.memset(buf, 0, ctypes.sizeof(buf))
+        lib.fa_debug_timeline(buf, n)
+        ghz = sorted(buf[4 * i + 3] / (buf[4 * i + 1] - buf[4 * i]) * 0.1 for i in range(n)
+                     if buf[4 * i + 1] > buf[4 * i] and buf[4 * i + 3] > 0)
+        rec = {"label": label, "workgroups_stamped": len(ghz)}
+        if ghz and cfg is not None:
+            rec.update({"ghz_in_kernel_median": round(ghz[len(ghz) // 2], 3),
+                        "ghz_p10": round(ghz[len(ghz) // 10], 3), "ghz_p90": round(ghz[9 * len(ghz) // 10], 3)})
+        print(json.dumps(rec), flush=True)
+        del q, k, v, o
+
+
 def per_dispatch(root, names):
     """{counter: [value per fa:: dispatch, in dispatch order]} and kernel ns per dispatch."""
     files = glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)
@@ -129,8 +180,11 @@ def per_dispatch(root, names):
     return {n: [per[n][d] for d in order] for n in per}, [dur[d] for d in order], [kname[d] for d in order]
 
 
-def summary(timing_jsonl, mfma_dir, fetch_dir, write_dir, out):
+def summary(timing_jsonl, mfma_dir, fetch_dir, write_dir, out, clocks_jsonl=None):
     timing = {json.loads(l)["label"]: json.loads(l) for l in open(timing_jsonl) if l.startswith("{")}
+    clk = {}
+    if clocks_jsonl and os.path.exists(clocks_jsonl):
+        clk = {json.loads(l)["label"]: json.loads(l) for l in open(clocks_jsonl) if l.startswith("{")}
     m, dur, kn = per_dispatch(mfma_dir, {"SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_MFMA", "GRBM_GUI_ACTIVE"})
     f, _, _ = per_dispatch(fetch_dir, {"FETCH_SIZE"})
     w, _, _ = per_dispatch(write_dir, {"WRITE_SIZE"})
@@ -155,9 +209,11 @@ def summary(timing_jsonl, mfma_dir, fetch_dir, write_dir, out):
             "mfma_busy": round(busy_frac, 4),
             "mfma_insts": nmf, "busy_cycles_per_mfma": round(busy / nmf, 2),
             "mfma_per_useful_flop": round(mfma_per_flop, 4),
-            "eff_clock_ghz_profiled": round(ghz, 3),
+            # GRBM_GUI_ACTIVE / time reads high below ~0.3 ms (guide DVFS note)
+            "eff_clock_ghz_profiled": round(ghz, 3) if mean(dur) >= 3e5 else None,
+            "ghz_in_kernel": clk.get(label, {}).get("ghz_in_kernel_median"),
             "ms_profiled": round(mean(dur) / 1e6, 4), "tflops_profiled": round(tf_prof, 1),
-            "identity": round(busy_frac * ghz * SIMDS * 1024 / mfma_per_flop / 1e3 / tf_prof, 3),
+
             "hbm_bytes": int(hbm), "alg_bytes": int(t["alg_bytes"]),
             "traffic_over_alg": round(hbm / t["alg_bytes"], 3),
             "hbm_gbs": round(hbm / (t["ms"] / 1e3) / 1e9, 1),
@@ -166,17 +222,20 @@ def summary(timing_jsonl, mfma_dir, fetch_dir, write_dir, out):
     with open(out, "w") as fo:
         for r in rows:
             fo.write(json.dumps(r) + "\n")
-    hdr = (f"{'shape':30s} {'tier':50s} {'TF/s':>7s} {'%peak':>6s} | {'TF/s pr':>7s} {'mfma':>6s} "
-           f"{'GHz pr':>6s} {'ident':>5s} | {'GB/s':>7s} {'tr/alg':>6s}")
+    hdr = (f"{'shape':30s} {'tier':50s} {'TF/s':>7s} {'%peak':>6s} {'GHz in-k':>8s} | {'TF/s pr':>7s} "
+           f"{'mfma':>6s} {'GHz pr':>6s} | {'GB/s':>7s} {'tr/alg':>6s}")
     print(hdr)
+    f2 = lambda x: "     —" if x is None else f"{x:6.2f}"
     for r in rows:
-        print(f"{r['label']:30s} {r['config']:50s} {r['tflops']:7.1f} {100*r['frac_nominal_peak']:6.1f} | "
-              f"{r['tflops_profiled']:7.1f} {100*r['mfma_busy']:6.1f} {r['eff_clock_ghz_profiled']:6.2f} "
-              f"{r['identity']:5.2f} | {r['hbm_gbs']:7.1f} {r['traffic_over_alg']:6.2f}")
+        print(f"{r['label']:30s} {r['config']:50s} {r['tflops']:7.1f} {100*r['frac_nominal_peak']:6.1f} "
+              f"{f2(r['ghz_in_kernel']):>8s} | {r['tflops_profiled']:7.1f} {100*r['mfma_busy']:6.1f} "
+              f"{f2(r['eff_clock_ghz_profiled'])} | {r['hbm_gbs']:7.1f} {r['traffic_over_alg']:6.2f}")
 
 
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run("--time" in sys.argv)
+    elif sys.argv[1] == "clocks":
+        clocks()
     else:
-        summary(*sys.argv[2:7])
+        summary(*sys.argv[2:8])

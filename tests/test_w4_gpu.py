@@ -66,17 +66,19 @@ SHAPES = [
 ]
 
 
-def _compare(b, h, s, causal, seed, scale=1.0, oracle_heads=True):
+def _compare(b, h, s, causal, seed, scale=1.0, oracle_heads=True, d=128, w4=W4, base_tier=BASE,
+             max_frac=2e-3):
     fa = _fa()
-    q, k, v = (_rand((b, h, s, 128), seed + i, scale if i < 2 else 1.0) for i in range(3))
-    base = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(BASE)[causal])
-    out = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(W4)[causal])
+    q, k, v = (_rand((b, h, s, d), seed + i, scale if i < 2 else 1.0) for i in range(3))
+    base = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(base_tier)[causal])
+    out = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(w4)[causal])
     torch.cuda.synchronize()
     assert torch.isfinite(out.float()).all()
     diff = (out.float() - base.float()).abs()
     assert diff.max().item() <= TOL, f"max diff vs ping-pong {diff.max().item()}"
     frac = (out != base).float().mean().item()
-    assert frac <= 2e-3, f"{frac:.2e} of the elements differ from the ping-pong"
+    if max_frac is not None:
+        assert frac <= max_frac, f"{frac:.2e} of the elements differ from the ping-pong"
     if oracle_heads:
         for flat in sorted({0, b * h // 2, b * h - 1}):
             bi, hi = divmod(flat, h)
@@ -162,3 +164,52 @@ def test_w4_second_item_chunk(b, h, s, causal):
     # starts cold -- ITEM/WARM reset, stale K/V images, the cross-item
     # epilogue deferral stopped at the first chunk's last item
     _compare(b, h, s, causal, seed=900)
+
+
+# head_dim 64: the same item program with 2-step QK^T chains, 4 O^T column
+# blocks per row block and register-staged K/V (rows of 128 B in HBM, the
+# images' 256-B slots half filled); against the head_dim-64 persistent
+# ping-pong (same arithmetic) and the oracle
+D64_W4 = "d64_" + W4
+D64_BASE = "d64_bm256_bn64_w8_m16_pingpong_persistent"
+D64_SHAPES = [(1, 8, 512), (2, 64, 2048), (3, 40, 1000), (1, 203, 300), (4, 50, 64), (1, 7, 4096),
+              (1, 32, 2048), (1, 72, 1024), (1, 4, 77)]
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", D64_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_w4_d64_matches_pingpong_and_oracle(shape, causal):
+    b, h, s = shape
+    # the persistent ping-pong runs a short non-causal last round as KV-pair
+    # halves (a different merge rounding): compare values, not bits, there
+    _compare(b, h, s, causal, seed=1000, d=64, w4=D64_W4, base_tier=D64_BASE,
+             max_frac=2e-3 if causal else None)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("s", [256, 1000, 2048])
+def test_w4_d64_peaked_rescale(s, causal):
+    _compare(1, 8, s, causal, seed=1100, scale=4.0, d=64, w4=D64_W4, base_tier=D64_BASE,
+             max_frac=2e-3 if causal else None)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("b,h,s", [(2100, 32, 64), (1, 2, 8192)])
+def test_w4_d64_long_and_second_chunk(b, h, s, causal):
+    _compare(b, h, s, causal, seed=1200, d=64, w4=D64_W4, base_tier=D64_BASE,
+             max_frac=2e-3 if causal else None)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", [(1, 8, 512), (3, 40, 1000), (1, 4, 77)], ids=lambda s: "x".join(map(str, s)))
+def test_w4_d64_bf16(shape, causal):
+    fa = _fa()
+    b, h, s = shape
+    q, k, v = (_rand((b, h, s, 64), 1300 + i).to(torch.bfloat16) for i in range(3))
+    out = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids("bf16_" + D64_W4)[causal])
+    torch.cuda.synchronize()
+    sc = q.float() @ k.float().transpose(-1, -2) / 64 ** 0.5
+    if causal:
+        sc = sc + torch.full((s, s), float("-inf"), device="cuda").triu(1)
+    ref = torch.softmax(sc, -1) @ v.float()
+    assert (out.float() - ref).abs().max().item() <= 5e-3
