@@ -655,11 +655,10 @@ static int launch_auto(int dtype, const void* q, const void* k, const void* v, v
   if (rc != FA_OK) return rc;
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
   const int sel = fa_select_config(batch, heads, seq_len, causal);
-  int id = twin(sel, dtype, head_dim);
-  // head_dim 64 of the W4 tier: the ping-pong persistent twin until the W4
-  // head_dim-64 program is measured on the GPU
-  if (sel >= 0 && kConfigs[sel].kind == 5 && head_dim == 64)
-    id = twin(cfg_for(256, 8, 64, causal ? 1 : 0, 1, 2), dtype, head_dim);
+  // (head_dim 64 of the W4 tier is the same item program with 2-step QK^T
+  // chains and register-staged K/V: +4-9 % over the 8-wave ping-pong at
+  // head_dim 64, profiles/r04_ab_w4_d64.jsonl)
+  const int id = twin(sel, dtype, head_dim);
   if (id < 0) return FA_ERR_BAD_CONFIG;
   return launch(id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
                 (hipStream_t)hip_stream);

@@ -351,8 +351,26 @@ def KF(slot):
 
 
 def VF(slot, half=None):
-    base = 144 + 4 * slot
+    base = 144 + 4 * slot if slot < 8 else 184 + 4 * (slot - 8)
     return R("v", base, 4) if half is None else R("v", base + 2 * half, 2)
+
+
+def v14():
+    """14 V^T fragment slots (the DMA build's free v184-v207 as slots 8-13):
+    all of PV(j)'s first-half fragments are read at the end of phase A, after
+    the last K reads, and six of the second half at the start of phase B,
+    before its exp2 stream (W4_XP=v14)"""
+    return "v14" in XP and dma()
+
+
+def vslot(f):
+    if v14():
+        return f if f < 14 else f - 14
+    return f % 8
+
+
+def vahead():
+    return 8 if v14() else V_AHEAD
 
 
 def KST(i):
@@ -408,6 +426,12 @@ QW, QM, NTILES, KVHI = "s88", "s89", "s90", "s91"  # this wave's first row, mask
 ITEM, WARM = "s92", "s93"   # item index; 1 if this item's Q, K(0), V(0), K(1) were prefetched
 
 
+def kslot(cb, t):
+    """K fragment slot of (key block cb, k-step t): two key blocks' fragments
+    at head_dim 128 (read one key block ahead), the whole tile's 8 at 64"""
+    return 4 * (cb & 1) + t if NT() == 4 else 2 * cb + t
+
+
 def k_read(t, cb, slot, kb):
     return dsr(f"ds_read_b128 {KF(slot)}, {KADDR[t]} offset:{kb + 4096 * cb}", KF(slot), KADDR[t])
 
@@ -459,7 +483,7 @@ def pv_mfmas():
             f = u * NE() + e
             frag_first[f] = len(ms)
             for b in range(4):
-                ms.append(mfma(O(b, e), VF(f % 8), P(b, u), O(b, e)))
+                ms.append(mfma(O(b, e), VF(vslot(f)), P(b, u), O(b, e)))
         for b in range(4):
             ms.append(mfma(L(b), ONES, P(b, u), L(b)))
     return ms, frag_first
@@ -613,7 +637,7 @@ def phase_a(st, p, with_max, diag=False):
                 mf += [ch[b][t] for b in range(4)]
     else:
         for x, (b, cb) in enumerate(chains):
-            slots = [4 * (cb & 1) + t for t in range(NT())]
+            slots = [kslot(cb, t) for t in range(NT())]
             mf += qk_chain(b, cb, slots)
     gaps = {}
 
@@ -628,7 +652,10 @@ def phase_a(st, p, with_max, diag=False):
     n = len(mf)
     # K reads of cb 0 first; the conversions of cb 0's four blocks cover
     # their LDS latency  (W4_XP=kpre, timing only: read in the previous phase B)
-    if "kpre" not in XP or diag or not with_max:
+    if NT() == 2:
+        # head_dim 64: all 8 fragments of the tile at once (the slots hold them)
+        put(0, [k_read(t, cb, kslot(cb, t), kb) for cb in range(4) for t in range(2)])
+    elif "kpre" not in XP or diag or not with_max:
         put(0, [k_read(t, 0, t, kb) for t in range(NT())])
     if diag:
         # blocks above the diagonal: P(j) out of them, then -inf
@@ -659,9 +686,9 @@ def phase_a(st, p, with_max, diag=False):
         # per chain of this cb)
         if "kspread" in XP and cb < 3 and not diag:
             put(4 * x + 1, k_read(b, cb + 1, 4 * ((cb + 1) & 1) + b, kb))
-        elif b == (cb if diag else 0) and cb < 3:
+        elif b == (cb if diag else 0) and cb < 3 and NT() == 4:
             for t in range(NT()):
-                put(NT() * x + 1 + t % 3, k_read(t, cb + 1, 4 * ((cb + 1) & 1) + t, kb))
+                put(NT() * x + 1 + t % 3, k_read(t, cb + 1, kslot(cb + 1, t), kb))
         # the running maxima of chain x - LAG (its MFMA results clear of the
         # 12-wait-state MFMA -> VALU window)
         if with_max and x >= lag() and "nomax" not in XP:
@@ -692,9 +719,9 @@ def phase_a(st, p, with_max, diag=False):
         for f in range(16):
             for i, r in enumerate(v_reads(f // 8, f % 8, f % 8, VBUF[p])):
                 put(6 + 3 * f + i, r)
-    for f in range(V_AHEAD):
-        for i, r in enumerate(v_reads(0, f, f, VBUF[p])):
-            put(n - 12 - 3 * (V_AHEAD - 3) + 3 * f + i, r)
+    for f in range(vahead()):
+        for i, r in enumerate(v_reads(0, f, vslot(f), VBUF[p])):
+            put(n - 12 - 3 * (vahead() - 3) + 3 * f + i, r)
     assert max(gaps) <= n, "every filler lands in a gap"
     st.interleave(mf, gaps)
     leftover = []
@@ -718,10 +745,19 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
         gaps.setdefault(k, []).extend(ins)
 
     # V fragments V_AHEAD ahead (the first V_AHEAD were read in phase A)
-    for f in range(V_AHEAD, 2 * NE() if not ("vinA" in XP and exps and dec_gap > 0) else V_AHEAD):
-        k = frag_first[f - V_AHEAD]
+    if v14():
+        # slots 8-13 are free: fragments 8-13 at once; 14, 15 into slots 0, 1
+        # once fragments 0, 1 have been consumed (MFMAs 0-7)
+        for f in range(8, 16):
+            u, e = divmod(f, NE())
+            r = v_reads(u, e, vslot(f), vb)
+            k = 2 * (f - 8) if f < 14 else 12 + 2 * (f - 14)
+            put(k, r[0])
+            put(k + 1, r[1])
+    for f in range(vahead(), 2 * NE() if not ("vinA" in XP and exps and dec_gap > 0 or v14()) else vahead()):
+        k = frag_first[f - vahead()]
         u, e = divmod(f, NE())
-        r = v_reads(u, e, f % 8, vb)
+        r = v_reads(u, e, vslot(f), vb)
         put(k + 1, r[0])
         put(k + 2, r[1])
     for i, ins in enumerate(leftover):
@@ -917,9 +953,9 @@ def qk_plain(st, kb):
     """QK^T of one tile, not interleaved (prologue)"""
     for cb in range(4):
         for t in range(NT()):
-            st.emit(k_read(t, cb, 4 * (cb & 1) + t, kb))
+            st.emit(k_read(t, cb, kslot(cb, t), kb))
         for b in range(4):
-            for m in qk_chain(b, cb, [4 * (cb & 1) + t for t in range(NT())]):
+            for m in qk_chain(b, cb, [kslot(cb, t) for t in range(NT())]):
                 st.emit(m)
 
 
@@ -930,7 +966,7 @@ def pv_plain(st, p):
     for f in range(2 * NE()):
         u, e = divmod(f, NE())
         k = frag_first[f - 2] + 1 if f >= 2 else 0
-        for i, r in enumerate(v_reads(u, e, f % 8, vb)):
+        for i, r in enumerate(v_reads(u, e, vslot(f), vb)):
             gaps.setdefault(k + i if f >= 2 else 0, []).append(r)
     st.interleave(mf, gaps)
 
@@ -1460,11 +1496,11 @@ def s0_with_epilogue(st):
     mf, gaps = [], {}
     for cb in range(4):
         for b in range(4):
-            mf += qk_chain(b, cb, [4 * (cb & 1) + t for t in range(NT())])
+            mf += qk_chain(b, cb, [kslot(cb, t) for t in range(NT())])
     gaps[0] = [k_read(t, 0, t, kb) for t in range(NT())]
     for cb in range(3):
         for t in range(NT()):
-            gaps.setdefault(4 * NT() * cb + 1 + t, []).append(k_read(t, cb + 1, 4 * ((cb + 1) & 1) + t, kb))
+            gaps.setdefault(4 * NT() * cb + 1 + t, []).append(k_read(t, cb + 1, kslot(cb + 1, t), kb))
     ops = epilogue_ops(False, ro=ROSAVE, rowbase=ROWSAVE, zero_o=True)
     n = len(mf)
     for i, op in enumerate(ops):
