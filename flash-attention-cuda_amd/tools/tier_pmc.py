@@ -147,12 +147,20 @@ def clocks():
             for _ in range(5):
                 fa.flash_attention_fwd(q, k, v, causal, out=o, config=cfg)
             torch.cuda.synchronize()
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
         fa.flash_attention_fwd(q, k, v, causal, out=o, config=cfg)
-        torch.cuda.synchronize()
+        en.record()
+        en.synchronize()
         ctypes.memset(buf, 0, ctypes.sizeof(buf))
         lib.fa_debug_timeline(buf, n)
-        ghz = sorted(buf[4 * i + 3] / (buf[4 * i + 1] - buf[4 * i]) * 0.1 for i in range(n)
-                     if buf[4 * i + 1] > buf[4 * i] and buf[4 * i + 3] > 0)
+        # the records persist across launches: keep this launch's (ending within
+        # its duration of the newest record; 100-MHz realtime ticks)
+        recs = [(buf[4 * i], buf[4 * i + 1], buf[4 * i + 3]) for i in range(n)
+                if buf[4 * i + 1] > buf[4 * i] and buf[4 * i + 3] > 0]
+        last = max((r[1] for r in recs), default=0)
+        win = st.elapsed_time(en) * 1e5 * 1.2 + 100
+        ghz = sorted(c / (t1 - t0) * 0.1 for t0, t1, c in recs if t1 >= last - win and t0 >= last - win)
         rec = {"label": label, "workgroups_stamped": len(ghz)}
         if ghz and cfg is not None:
             rec.update({"ghz_in_kernel_median": round(ghz[len(ghz) // 2], 3),
