@@ -1519,6 +1519,12 @@ def generate(causal, split=False):
     # the workgroup's items (a chunk of fa_w4_kernel.hpp's table) in one
     # statement, so the next item's operands can be loaded in this one's
     # last iteration
+    # code-placement experiment (MI355X_MICROARCH.md, two waves per SIMD,
+    # item 8): W4_XP=shiftN moves the whole program by N bytes
+    for x in XP:
+        if x.startswith("shift"):
+            for _ in range(int(x[5:]) // 4):
+                st.raw("s_nop 0")
     st.raw(f"s_mov_b32 {ITEM}, 0")
     st.raw(f"s_mov_b32 {WARM}, 0")
     if dma():
