@@ -79,7 +79,15 @@ def set_dtype(bf16):
               if bf16 else {"mfma": "v_mfma_f32_16x16x32_f16", "cvt_pk": "v_cvt_pk_f16_f32",
                             "one2": "0x3c003c00"})
     DT["bf16"] = bf16
+# V^T fragments read this many fragments ahead of their PV MFMAs (4 or 5:
+# level within noise at both head_dims, profiles/r04_ab_w4_wait_coalescing*)
 V_AHEAD = int(os.environ.get("W4_V_AHEAD", "3"))
+# counted-wait coalescing: a wait for one LDS read also retires the younger
+# reads issued at least WAGE wait states earlier (0: wait for the needed read
+# only), so their own first uses need no wait of their own -- half the
+# s_waitcnt of a tile, +0.8-1.3 % (profiles/r04_ab_w4_wait_coalescing*.jsonl;
+# stamps: tile 2929 -> 2878 cycles, r04_w4_stamps_wait_coalescing.txt)
+WAGE = int(os.environ.get("W4_WAGE", "8"))
 
 # head_dim of the generated function (set_hd): 128, the reference's, or 64.
 # Q/K/V/O rows are 2*hd bytes in HBM; the LDS images keep 256-B row slots at
@@ -194,7 +202,7 @@ class Stream:
         self.mfma_w = {}   # reg -> pos of the last MFMA write
         self.valu_w = {}   # reg -> pos of the last VALU write
         self.trans_w = {}  # reg -> pos of the last transcendental write
-        self.lgkm = []     # outstanding LDS ops, oldest first: set of dst regs (reads) or None
+        self.lgkm = []     # outstanding LDS ops, oldest first: (set of dst regs or None, pos)
         self.pending = {}  # label -> list of saved states
         self.dead = False  # after an unconditional branch
 
@@ -256,12 +264,14 @@ class Stream:
         """counted lgkmcnt so every outstanding LDS read writing a needed reg is done"""
         need = set(regs_needed)
         last = -1
-        for i, op in enumerate(self.lgkm):
+        for i, (op, _) in enumerate(self.lgkm):
             if op is not None and op & need:
                 last = i
         if last < 0:
             return
         after = len(self.lgkm) - 1 - last
+        if WAGE:
+            after = sum(1 for _, at in self.lgkm[last + 1:] if at > self.pos - WAGE)
         self.raw(f"s_waitcnt lgkmcnt({min(after, 15)})")
         keep = min(after, 15)
         self.lgkm = self.lgkm[len(self.lgkm) - keep:]
@@ -317,7 +327,7 @@ class Stream:
                 self.mfma_w.pop(r, None)
                 self.valu_w.pop(r, None)
         if k in ("dsr", "dsw"):
-            self.lgkm.append(set(ins.w) if ins.lgkm_dst else None)
+            self.lgkm.append((set(ins.w) if ins.lgkm_dst else None, self.pos - 1))
 
     def interleave(self, mfmas, gaps):
         """gaps[k] = fillers issued before mfmas[k]; gaps[len(mfmas)] after the last"""
@@ -720,7 +730,7 @@ def phase_a(st, p, with_max, diag=False):
             for i, r in enumerate(v_reads(f // 8, f % 8, f % 8, VBUF[p])):
                 put(6 + 3 * f + i, r)
     for f in range(vahead()):
-        for i, r in enumerate(v_reads(0, f, vslot(f), VBUF[p])):
+        for i, r in enumerate(v_reads(*divmod(f, NE()), vslot(f), VBUF[p])):
             put(n - 12 - 3 * (vahead() - 3) + 3 * f + i, r)
     assert max(gaps) <= n, "every filler lands in a gap"
     st.interleave(mf, gaps)

@@ -74,7 +74,10 @@ def run(time_it):
     g = torch.Generator(device="cuda")
     g.manual_seed(7)
     names = {c.name: c.id for c in fa.configs()}
+    only = set(os.environ.get("FA_TIER_ONLY", "").split(",")) - {""}
     for label, b, h, s, causal, *forced in SHAPES:
+        if only and label not in only:
+            continue
         shape = (b, h, s, 128)
         q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5, generator=g)
                    for _ in range(3))
