@@ -509,6 +509,11 @@ STAGE2 = "stage1" not in XP
 LD_AT = int(os.environ.get("W4_LD_AT", "18"))
 LD_SP = int(os.environ.get("W4_LD_SP", "2"))
 DMA_AT = int(os.environ.get("W4_DMA_AT", "2"))  # first phase-A gap of the DMA sequence
+# gap of a chain's maxima within chain x + LAG, and the first phase-B gap of
+# phase A's leftover maxima: one gap later than the hazard windows need
+# spares 3 of a tile's 5 s_nop (profiles/r04_ab_w4_nop_trim*.jsonl)
+MAX_OFF = int(os.environ.get("W4_MAX_OFF", "2"))
+LEFT_OFF = int(os.environ.get("W4_LEFT_OFF", "3"))
 
 
 # K/V staging by LDS-DMA (the default; W4_XP=regstage: the round-3 register
@@ -705,8 +710,9 @@ def phase_a(st, p, with_max, diag=False):
             y = x - lag()
             by, cby = chains[y]
             mm = max_block(by, cby, first=(cby == 0 and by in (0, 2)))
-            put(NT() * x + 1, mm[0])
-            put(NT() * x + 2, mm[1])
+            mo = MAX_OFF
+            put(NT() * x + mo, mm[0])
+            put(min(NT() * x + mo + 1, n), mm[1])
     # stage traffic: LDS writes in cb 0, loads in cb 1
     if "nostage" not in XP and dma():
         for i, ld in enumerate(stage_loads(p=p)):
@@ -771,7 +777,7 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
         put(k + 1, r[0])
         put(k + 2, r[1])
     for i, ins in enumerate(leftover):
-        put(1 + i, ins)
+        put(LEFT_OFF + i, ins)
     if "kpre" in XP and exps:  # timing only: next phase A's cb-0 K fragments (stale buffer)
         for t in range(4):
             put(len(mf) - 12 + 2 * t, k_read(t, 0, t, KBUF[p]))
@@ -1489,7 +1495,8 @@ def epilogue_ops(split, ro=RO, rowbase=ST1, zero_o=False):
             pol = OPOL if not split else " sc1"
             E(vmem(f"buffer_store_dwordx4 v[152:155], {T[7]}, {ro}, 0 offen offset:{64 * ep}{pol}",
                    r=["v[152:155]", T[7]]))
-            E("s_nop 1")
+            # (no pad: the next write of v[152:155] is the next pair's
+            # conversion, 20+ instructions on)
     E("s_nop 1")
     return ops
 
