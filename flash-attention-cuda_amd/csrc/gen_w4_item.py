@@ -136,6 +136,14 @@ PF_BEFORE_DRAIN = os.environ.get("W4_PF_BEFORE", "0") == "1"  # V^T fragments re
 # register; its O descriptor and row base wait in s[60:63] / s64
 XOVL = os.environ.get("W4_XOVL", "1") == "1" and DIAG not in ("stamps", "pstamps")  # (s60-s69: stamps)
 ROSAVE, ROWSAVE = "s[60:63]", "s64"
+# the deferred epilogue zeroes O / l with 32x32x16 MFMAs of zero operands
+# instead of v_accvgpr_write: at head_dim 64 (+0.3-2.5 %); at 128 the writes
+# stay (the MFMAs measured -0.1-0.2 %, profiles/r04_ab_w4_mfma_zeroing*.jsonl)
+MFZ_XP = "nomfz" not in XP
+
+
+def mfz():
+    return MFZ_XP and HDC["hd"] == 64
 # cache policy of the (non-split) O stores; the split tier's slab stores stay
 # sc1 (read by other workgroups)
 OPOL = " ".join([""] + os.environ.get("W4_OPOL", "sc1").split("+"))  # e.g. W4_OPOL=nt, sc1+nt, ""
@@ -509,6 +517,7 @@ STAGE2 = "stage1" not in XP
 LD_AT = int(os.environ.get("W4_LD_AT", "18"))
 LD_SP = int(os.environ.get("W4_LD_SP", "2"))
 DMA_AT = int(os.environ.get("W4_DMA_AT", "2"))  # first phase-A gap of the DMA sequence
+DMA_SP = int(os.environ.get("W4_DMA_SP", "1"))  # gaps between its instructions
 # gap of a chain's maxima within chain x + LAG, and the first phase-B gap of
 # phase A's leftover maxima: one gap later than the hazard windows need
 # spares 3 of a tile's 5 s_nop (profiles/r04_ab_w4_nop_trim*.jsonl)
@@ -716,7 +725,7 @@ def phase_a(st, p, with_max, diag=False):
     # stage traffic: LDS writes in cb 0, loads in cb 1
     if "nostage" not in XP and dma():
         for i, ld in enumerate(stage_loads(p=p)):
-            put((4 + i) if diag else (DMA_AT + i), ld)
+            put((4 + i) if diag else (DMA_AT + DMA_SP * i), ld)
     elif "nostage" not in XP and STAGE2:
         for i, ld in enumerate(stage_loads(1 - p)):
             if HDC["hd"] == 128:
@@ -1443,7 +1452,7 @@ def epilogue_ops(split, ro=RO, rowbase=ST1, zero_o=False):
     for b in range(4):
         l, inv = T[0], T[1]
         E(valu(f"v_accvgpr_read_b32 {l}, {L(b, 0)}", r=[L(b, 0)], w=[l]))
-        if zero_o:
+        if zero_o and not mfz():
             for i in range(4):
                 E(valu(f"v_accvgpr_write_b32 {L(b, i)}, 0", w=[L(b, i)]))
         # inv = l > 0 ? 1.0f / l : 0  (IEEE division, the compiler's sequence)
@@ -1478,7 +1487,7 @@ def epilogue_ops(split, ro=RO, rowbase=ST1, zero_o=False):
                 for i in range(4):
                     src = L(b, i) if DIAG == "l" else O(b, e, i)
                     E(valu(f"v_accvgpr_read_b32 {d[4 * x + i]}, {src}", r=[src], w=[d[4 * x + i]]))
-                    if zero_o:
+                    if zero_o and not mfz():
                         E(valu(f"v_accvgpr_write_b32 {O(b, e, i)}, 0", w=[O(b, e, i)]))
                 if DIAG in ("raw", "l"):
                     continue
@@ -1497,8 +1506,23 @@ def epilogue_ops(split, ro=RO, rowbase=ST1, zero_o=False):
                    r=["v[152:155]", T[7]]))
             # (no pad: the next write of v[152:155] is the next pair's
             # conversion, 20+ instructions on)
+        if zero_o and mfz():
+            # this row block's O (and, after the last one, every l) zeroed by
+            # 32x32x16 MFMAs of zero operands (v96-99 = 0 here): 16 AGPRs per
+            # instruction on the otherwise idle matrix pipe
+            for z in range(0, 4 * NE(), 16):
+                E(zero_mfma(4 * NE() * b + z))
+            if b == 3:
+                E(zero_mfma(128))
     E("s_nop 1")
     return ops
+
+
+def zero_mfma(a0):
+    """a[a0:a0+15] = 0 by one 32x32x16 MFMA (A = B = v[96:99] = 0, C = 0)"""
+    op = "v_mfma_f32_32x32x16_" + ("bf16" if DT["bf16"] else "f16")
+    return Ins(f"{op} a[{a0}:{a0 + 15}], v[96:99], v[96:99], 0", "mfma",
+               r=["v[96:99]"], w=[f"a[{a0}:{a0 + 15}]"])
 
 
 def epilogue(st, split):
