@@ -493,7 +493,7 @@ def exp_ops():
     return [valu(f"v_exp_f32 v{x}, v{x}", r=[f"v{x}"], w=[f"v{x}"], kind="trans") for x in range(64)]
 
 
-def pv_mfmas():
+def pv_mfmas(rowsums=True):
     """PV + row sums in M16::pv order: for u: for e: 4 b; then 4 row sums"""
     ms, frag_first = [], {}
     for u in range(2):
@@ -502,9 +502,13 @@ def pv_mfmas():
             frag_first[f] = len(ms)
             for b in range(4):
                 ms.append(mfma(O(b, e), VF(vslot(f)), P(b, u), O(b, e)))
-        for b in range(4):
-            ms.append(mfma(L(b), ONES, P(b, u), L(b)))
+        if rowsums:
+            ms += rowsum_mfmas(u)
     return ms, frag_first
+
+
+def rowsum_mfmas(u):
+    return [mfma(L(b), ONES, P(b, u), L(b)) for b in range(4)]
 
 
 # Staging sets: stage j's K/V rows live in set j & 1 between their global
@@ -679,6 +683,14 @@ def phase_a(st, p, with_max, diag=False):
     if NT() == 2:
         # head_dim 64: all 8 fragments of the tile at once (the slots hold them)
         put(0, [k_read(t, cb, kslot(cb, t), kb) for cb in range(4) for t in range(2)])
+    elif "rsA" in XP and with_max and not diag:
+        # timing only: the previous PV's row sums ahead of this QK^T, under
+        # the cb-0 K reads' latency
+        for t in range(NT()):
+            st.emit(k_read(t, 0, t, kb))
+        for u in range(2):
+            for m in rowsum_mfmas(u):
+                st.emit(m)
     elif "kpre" not in XP or diag or not with_max:
         put(0, [k_read(t, 0, t, kb) for t in range(NT())])
     if diag:
@@ -760,7 +772,7 @@ def phase_a(st, p, with_max, diag=False):
 def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
     """PV(j) from vbuf[j&1]; decision at dec_gap; exp2 of S(j+1) after it"""
     vb = VBUF[p]
-    mf, frag_first = pv_mfmas()
+    mf, frag_first = pv_mfmas(rowsums=not ("rsA" in XP and dec_gap > 0 and exps))
     gaps = {}
 
     def put(k, ins):

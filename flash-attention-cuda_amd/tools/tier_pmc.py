@@ -58,7 +58,14 @@ SHAPES = [  # (label, batch, heads, seq, causal[, forced tier name | "auto"])
     ("bn128_s8192_noncausal", 1, 32, 8192, False, "bm128_bn128_w4_m16_noncausal"),
     ("bn128_s8192_causal", 1, 32, 8192, True, "bm128_bn128_w4_m16_causal"),
     ("pingpong_item_s8192_causal", 1, 32, 8192, True, "bm256_bn64_w8_m16_pingpong_causal"),
+    # head_dim 64 (label prefix d64_: the dispatcher's d64 twin, W4 on these)
+    ("d64_target_s8192_causal", 1, 32, 8192, True, "auto"),
+    ("d64_headline_b64_s4096_causal", 64, 32, 4096, True, "auto"),
 ]
+
+
+def hd_of(label):
+    return 64 if label.startswith("d64_") else 128
 ITERS = 6
 PEAK = 2516.6  # TFLOP/s, 256 CU x 2.4 GHz x 4096 FLOP/clk/CU
 SIMDS = 1024
@@ -78,13 +85,14 @@ def run(time_it):
     for label, b, h, s, causal, *forced in SHAPES:
         if only and label not in only:
             continue
-        shape = (b, h, s, 128)
+        hd = hd_of(label)
+        shape = (b, h, s, hd)
         q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5, generator=g)
                    for _ in range(3))
         o = torch.empty_like(q)
         cfg = (None if forced[0] == "auto" else names[forced[0]]) if forced else fa.select_config(b, h, s, causal)
         fwd = lambda: fa.flash_attention_fwd(q, k, v, causal, out=o, config=cfg)
-        flops = fa.attention_flops(b, h, s, 128, causal)
+        flops = fa.attention_flops(b, h, s, hd, causal)
         torch.cuda.synchronize()
         if time_it:
             for _ in range(3):
@@ -102,10 +110,11 @@ def run(time_it):
             ms = sorted(best)[1]
             print(json.dumps({"label": label, "batch": b, "heads": h, "seq": s, "causal": causal,
                               "config": (fa.configs()[cfg].name if cfg is not None else
+                                         "auto_d64 (W4 d64 twin)" if hd == 64 else
                                          "split_T%d" % fa.load_library().fa_fwd_split_pieces(b, h, s, 128, int(causal))),
                               "ms": ms,
                               "tflops": flops / (ms / 1e3) / 1e12, "flops": flops,
-                              "alg_bytes": 8.0 * b * h * s * 128}), flush=True)
+                              "alg_bytes": 8.0 * b * h * s * hd}), flush=True)
         else:
             for _ in range(ITERS):
                 fwd()
@@ -138,7 +147,7 @@ def clocks():
     n = 4096
     buf = (ctypes.c_ulonglong * (4 * n))()
     for label, b, h, s, causal, *forced in SHAPES:
-        shape = (b, h, s, 128)
+        shape = (b, h, s, hd_of(label))
         q, k, v = (torch.empty(shape, dtype=torch.float16, device="cuda").uniform_(-0.5, 0.5, generator=g)
                    for _ in range(3))
         o = torch.empty_like(q)
