@@ -23,7 +23,9 @@ Derived per launch (first launch of each shape dropped):
                 this is below the un-profiled HIP-event TFLOP/s)
   ghz_in_kernel = s_memtime cycles / s_memrealtime time per workgroup, median,
                 from the stamps build after >= 2 s of launches (tier_pmc.py
-                clocks); eff_clock is left out below 0.3 ms, where it reads high
+                clocks), W4 rows only (the other tiers' stamps builds stamp
+                every loop phase); eff_clock is left out below 0.3 ms, where it
+                reads high, and above 2.4 GHz
   frac_nominal = TFLOP/s (un-profiled, HIP events) / 2516.6
   hbm_gbs     = (FETCH + WRITE bytes) / un-profiled time
 """
@@ -229,9 +231,14 @@ def summary(timing_jsonl, mfma_dir, fetch_dir, write_dir, out, clocks_jsonl=None
             "mfma_busy": round(busy_frac, 4),
             "mfma_insts": nmf, "busy_cycles_per_mfma": round(busy / nmf, 2),
             "mfma_per_useful_flop": round(mfma_per_flop, 4),
-            # GRBM_GUI_ACTIVE / time reads high below ~0.3 ms (guide DVFS note)
-            "eff_clock_ghz_profiled": round(ghz, 3) if mean(dur) >= 3e5 else None,
-            "ghz_in_kernel": clk.get(label, {}).get("ghz_in_kernel_median"),
+            # GRBM_GUI_ACTIVE / time reads high below ~0.3 ms (guide DVFS note);
+            # a quotient above the 2.4 GHz maximum is a counter artefact, not a clock
+            "eff_clock_ghz_profiled": round(ghz, 3) if mean(dur) >= 3e5 and ghz <= 2.4 else None,
+            # in-kernel clocks only where the stamps build adds no stamps inside
+            # the loop (W4: one start / end record per workgroup); the other
+            # tiers' diagnostic builds stamp every phase, which moves their clock
+            "ghz_in_kernel": (clk.get(label, {}).get("ghz_in_kernel_median")
+                              if "asm_persistent" in t["config"] else None),
             "ms_profiled": round(mean(dur) / 1e6, 4), "tflops_profiled": round(tf_prof, 1),
 
             "hbm_bytes": int(hbm), "alg_bytes": int(t["alg_bytes"]),
