@@ -772,7 +772,7 @@ def phase_a(st, p, with_max, diag=False):
 def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
     """PV(j) from vbuf[j&1]; decision at dec_gap; exp2 of S(j+1) after it"""
     vb = VBUF[p]
-    mf, frag_first = pv_mfmas(rowsums=not ("rsA" in XP and dec_gap > 0 and exps))
+    mf, frag_first = pv_mfmas(rowsums=not ("rsA" in XP and dec_gap > 0 and exps) and "norowsum" not in XP)
     gaps = {}
 
     def put(k, ins):

@@ -19,8 +19,9 @@ ap.add_argument("--batch", type=int, default=64)
 ap.add_argument("--heads", type=int, default=32)
 ap.add_argument("--seq", type=int, default=4096)
 ap.add_argument("--causal", action="store_true")
+ap.add_argument("--lib", default="stamps", help="lib/libfa_mi355x_<lib>.so, an FA_STAMPS build")
 a = ap.parse_args()
-fa.LIB_PATH = os.path.join(HERE, "lib", "libfa_mi355x_stamps.so")
+fa.LIB_PATH = os.path.join(HERE, "lib", f"libfa_mi355x_{a.lib}.so")
 lib = fa.load_library()
 lib.fa_debug_timeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
 shape = (a.batch, a.heads, a.seq, 128)

@@ -10,5 +10,5 @@ name=$1; envs=$2
 tmp=$(mktemp -d)
 trap 'rm -rf "$tmp"' EXIT
 env -u W4_DIAG -u W4_XP -u W4_OPOL -u W4_WAGE -u W4_V_AHEAD -u W4_MAX_OFF -u W4_LEFT_OFF -u W4_DMA_AT -u W4_DMA_SP $envs python3 csrc/gen_w4_item.py "$tmp/fa_w4_item.inc"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-honor-nans -I"$tmp" -I../include -Icsrc \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-honor-nans ${W4_HIPFLAGS:-} -I"$tmp" -I../include -Icsrc \
   -shared csrc/fa_fwd.hip csrc/flash_attention_v9.cpp -o lib/libfa_mi355x_$name.so
