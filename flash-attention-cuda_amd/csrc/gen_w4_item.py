@@ -522,6 +522,7 @@ LD_AT = int(os.environ.get("W4_LD_AT", "18"))
 LD_SP = int(os.environ.get("W4_LD_SP", "2"))
 DMA_AT = int(os.environ.get("W4_DMA_AT", "2"))  # first phase-A gap of the DMA sequence
 DMA_SP = int(os.environ.get("W4_DMA_SP", "1"))  # gaps between its instructions
+CVT0 = "cvt0" in XP
 # gap of a chain's maxima within chain x + LAG, and the first phase-B gap of
 # phase A's leftover maxima: one gap later than the hazard windows need
 # spares 3 of a tile's 5 s_nop (profiles/r04_ab_w4_nop_trim*.jsonl)
@@ -704,6 +705,11 @@ def phase_a(st, p, with_max, diag=False):
         c = cvt_block(b, cb)
         if "nocvt" in XP:
             pass
+        elif CVT0 and not diag and NT() == 4:
+            # every conversion ahead of the first MFMA, under the cb-0 K
+            # reads' LDS latency (the registers they read were written by the
+            # previous phase B's exp2; the chains overwrite them later)
+            put(0, c)
         elif x < 4 or ("tmajor" in XP and b > 0):
             put(4 * (x - b) if x >= 4 else 0, c)
         elif "tmajor" in XP:
