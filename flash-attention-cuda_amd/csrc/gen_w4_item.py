@@ -523,6 +523,7 @@ LD_SP = int(os.environ.get("W4_LD_SP", "2"))
 DMA_AT = int(os.environ.get("W4_DMA_AT", "2"))  # first phase-A gap of the DMA sequence
 DMA_SP = int(os.environ.get("W4_DMA_SP", "1"))  # gaps between its instructions
 CVT0 = "cvt0" in XP
+CVT_EARLY = "cvtearly" in XP
 # gap of a chain's maxima within chain x + LAG, and the first phase-B gap of
 # phase A's leftover maxima: one gap later than the hazard windows need
 # spares 3 of a tile's 5 s_nop (profiles/r04_ab_w4_nop_trim*.jsonl)
@@ -715,6 +716,11 @@ def phase_a(st, p, with_max, diag=False):
         elif "tmajor" in XP:
             put(4 * x - 2, c[0])
             put(4 * x - 1, c[1])
+        elif CVT_EARLY and NT() == 4 and not diag:
+            # the first conversion two gaps earlier, into the chain's empty
+            # gap: one filler per gap (maxima at +2 / +3, conversions at +1 / +4)
+            put(NT() * x - 3, c[0])
+            put(NT() * x, c[1])
         else:
             put(NT() * x - 1, c[0])
             put(NT() * x, c[1])

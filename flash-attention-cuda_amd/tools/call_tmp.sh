@@ -1,7 +1,10 @@
 #!/bin/bash
-# un-instrumented workgroup cycles (FA_STAMPS build: start/end records only) -> cycles per tile
+# conversions spread one per gap (cvtearly): A/B, d64 A/B, stamps
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-/root/repo}/flash-attention-cuda_amd"
-timeout -k 10 120 python tools/clock_check.py --batch 1 --seq 8192 2>&1 | grep -v amdgpu.ids &&
-timeout -k 10 120 python tools/clock_check.py --batch 1 --seq 8192 --causal 2>&1 | grep -v amdgpu.ids &&
-timeout -k 10 120 python tools/clock_check.py --batch 64 --seq 4096 --causal 2>&1 | grep -v amdgpu.ids
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+VARS="ce" OUT=ce bash flash-attention-cuda_amd/tools/ab_vars.sh > gpurun_out/ce.txt 2>&1 || exit 1
+grep -v amdgpu.ids gpurun_out/ce.txt
+cd flash-attention-cuda_amd
+for v in s_base s_ce; do
+timeout -k 10 60 python tools/w4_stamps.py --config 38 --seq 8192 --lib $v 2>&1 | grep -v amdgpu.ids || exit 1
+done
