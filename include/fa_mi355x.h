@@ -152,7 +152,8 @@ int fa_fwd_bf16_ws(const void* q, const void* k, const void* v, void* o,
  *
  * Config ids are positions in this build's table (fa_num_configs /
  * fa_config_info): they are not stable across releases (round 3 renumbered
- * 0-49 to 0-43 when the table was trimmed to the dispatched tiers).  Select a
+ * 0-49 to 0-43 when the table was trimmed to the dispatched tiers; round 4
+ * appended the head_dim-64 W4 configs 44-47).  Select a
  * tier by its fa_config_info().name, not by a remembered id. */
 int fa_select_config(int batch, int heads, int seq_len, int causal);
 
