@@ -524,6 +524,9 @@ DMA_AT = int(os.environ.get("W4_DMA_AT", "2"))  # first phase-A gap of the DMA s
 DMA_SP = int(os.environ.get("W4_DMA_SP", "1"))  # gaps between its instructions
 CVT0 = "cvt0" in XP
 CVT_EARLY = "cvtearly" in XP
+# the 8 row-sum MFMAs of PV(j) at the start of phase A(j+1), under the K
+# reads' latency, instead of at the end of the exp2-bound phase B(j)
+RSA = "rsa" in XP
 # gap of a chain's maxima within chain x + LAG, and the first phase-B gap of
 # phase A's leftover maxima: one gap later than the hazard windows need
 # spares 3 of a tile's 5 s_nop (profiles/r04_ab_w4_nop_trim*.jsonl)
@@ -541,6 +544,7 @@ LEFT_OFF = int(os.environ.get("W4_LEFT_OFF", "3"))
 # and waited for (vmcnt(0)) before the iteration's barrier.
 DMA_ON = "regstage" not in XP
 SM0 = "s70"          # M0 of the enclosing code, restored at the end
+PEND = "s71"         # 1: the last phase B's row sums are pending (RSA)
 
 
 def dma():
@@ -682,19 +686,17 @@ def phase_a(st, p, with_max, diag=False):
     n = len(mf)
     # K reads of cb 0 first; the conversions of cb 0's four blocks cover
     # their LDS latency  (W4_XP=kpre, timing only: read in the previous phase B)
-    if NT() == 2:
-        # head_dim 64: all 8 fragments of the tile at once (the slots hold them)
-        put(0, [k_read(t, cb, kslot(cb, t), kb) for cb in range(4) for t in range(2)])
-    elif "rsA" in XP and with_max and not diag:
-        # timing only: the previous PV's row sums ahead of this QK^T, under
-        # the cb-0 K reads' latency
-        for t in range(NT()):
-            st.emit(k_read(t, 0, t, kb))
-        for u in range(2):
-            for m in rowsum_mfmas(u):
-                st.emit(m)
-    elif "kpre" not in XP or diag or not with_max:
-        put(0, [k_read(t, 0, t, kb) for t in range(NT())])
+    # (head_dim 64: all 8 fragments of the tile at once, the slots hold them)
+    k0 = ([k_read(t, cb, kslot(cb, t), kb) for cb in range(4) for t in range(2)] if NT() == 2
+          else [k_read(t, 0, t, kb) for t in range(NT())])
+    if RSA:
+        # the previous PV's row sums, deferred by its phase B's fast path,
+        # ahead of this QK^T under the cb-0 K reads' latency
+        for ins in k0:
+            st.emit(ins)
+        flush_rowsums(st)
+    elif NT() == 2 or "kpre" not in XP or diag or not with_max:
+        put(0, k0)
     if diag:
         # blocks above the diagonal: P(j) out of them, then -inf
         above = [(b, cb) for cb in range(4) for b in range(4) if cb > b]
@@ -784,7 +786,7 @@ def phase_a(st, p, with_max, diag=False):
 def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
     """PV(j) from vbuf[j&1]; decision at dec_gap; exp2 of S(j+1) after it"""
     vb = VBUF[p]
-    mf, frag_first = pv_mfmas(rowsums=not ("rsA" in XP and dec_gap > 0 and exps) and "norowsum" not in XP)
+    mf, frag_first = pv_mfmas(rowsums=not (RSA and exps) and "norowsum" not in XP)
     gaps = {}
 
     def put(k, ins):
@@ -852,6 +854,8 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
         st.emit(f)
     if not exps:
         return mf, gaps
+    if RSA:
+        st.raw(f"s_mov_b32 {PEND}, 1")  # this PV's row sums: the next phase A
     if dec_gap > 0:
         stamp(st, 60)
         stamp_acc(st, 65, 60, 62)
@@ -873,11 +877,31 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
                 if isinstance(f, str) or f.kind != "trans":
                     st.emit(f)
         st.emit(mf[k])
+    if RSA:
+        # l takes this PV's row sums before the rescale scales it
+        for u in range(2):
+            for m in rowsum_mfmas(u):
+                st.emit(m)
     slow_softmax(st, first=False)
     for e in exp_ops():
         st.emit(e)
     st.branch("s_branch", label_end)
     return mf, gaps
+
+
+def flush_rowsums(st):
+    """the row sums a phase B's fast path left pending (PEND = 1): the
+    previous P is still in v64-95 (this phase's conversions follow)"""
+    if not RSA:
+        return
+    skip = newlabel("nors")
+    st.raw(f"s_cmp_eq_u32 {PEND}, 0")
+    st.branch("s_cbranch_scc1", skip)
+    for u in range(2):
+        for m in rowsum_mfmas(u):
+            st.emit(m)
+    st.label(skip)
+    st.raw(f"s_mov_b32 {PEND}, 0")
 
 
 def row_max_b(st, b, dst):
@@ -1061,6 +1085,7 @@ def body(st, p, causal, labels):
     phase_b(st, p, [], dec_gap=0, label_slow=L["slow2"][p], label_end=L["end"][p])
     # ---- drain (j = n_w - 1: PV only) / idle (j >= n_w: staging only) ----
     st.label(L["notsteady"][p])
+    flush_rowsums(st)  # before the drain's conversions overwrite that P
     st.raw(f"s_cmp_eq_u32 {SJ1}, {NTILES}")
     st.branch("s_cbranch_scc1", L["last"][p])
     if dma():
@@ -1451,6 +1476,8 @@ def prologue(st, causal, split=False):
     st.raw("s_barrier")
     prostamp(st, 4)  # -> V(0), K(1) written, loop start
     pstamp(st, 62)
+    if RSA:
+        st.raw(f"s_mov_b32 {PEND}, 0")
     st.raw(f"s_mov_b32 {SJ}, 0")
     if DIAG == "stamps":
         for r in range(64, 68):

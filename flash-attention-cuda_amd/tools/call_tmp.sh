@@ -1,6 +1,20 @@
 #!/bin/bash
-# the new seeded random-shape W4 parity tests
+# deferred row sums (W4_XP=rsa): W4/d64/split GPU tests on the variant, then A/B
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-timeout -k 10 600 python -u -m pytest tests/test_w4_gpu.py -k random -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_random.log 2>&1
-rc=$?; tail -25 gpurun_out/pytest_random.log; exit $rc
+L=flash-attention-cuda_amd/lib
+cp $L/libfa_mi355x.so /tmp/prod_keep.so && cp $L/libfa_mi355x_rsa.so $L/libfa_mi355x.so &&
+timeout -k 10 400 python -u -m pytest tests/test_w4_gpu.py tests/test_d64_gpu.py tests/test_split_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_rsa.log 2>&1
+rc=$?; cp /tmp/prod_keep.so $L/libfa_mi355x.so; tail -3 gpurun_out/pytest_rsa.log; [ $rc -eq 0 ] || exit $rc
+VARS="rsa" OUT=rsa2 bash flash-attention-cuda_amd/tools/ab_vars.sh > gpurun_out/rsa2.txt 2>&1 || exit 1
+AB="timeout -k 10 300 python flash-attention-cuda_amd/tools/ab.py --configs auto --libs prod,rsa --head-dim 64"
+O=gpurun_out/ab_rsa2_d64.jsonl
+$AB --seq 8192 --causal --rounds 5 --iters 20 > $O &&
+$AB --seq 4096 --batch 64 --causal --rounds 5 --iters 10 >> $O || exit 1
+grep -v amdgpu.ids gpurun_out/rsa2.txt
+python - $O <<'PY'
+import json, sys
+for l in open(sys.argv[1]):
+    r = json.loads(l)
+    print(f'd64 {r["lib"]:>8} B={r["batch"]:<3} S={r["seq"]:<6} {"c " if r["causal"] else "nc"} {r["median_tflops"]:8.1f}')
+PY
