@@ -1,20 +1,12 @@
 #!/bin/bash
-# deferred row sums (W4_XP=rsa): W4/d64/split GPU tests on the variant, then A/B
+# run-to-run spread of the bench line on one box (three back-to-back processes)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-L=flash-attention-cuda_amd/lib
-cp $L/libfa_mi355x.so /tmp/prod_keep.so && cp $L/libfa_mi355x_rsa.so $L/libfa_mi355x.so &&
-timeout -k 10 400 python -u -m pytest tests/test_w4_gpu.py tests/test_d64_gpu.py tests/test_split_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_rsa.log 2>&1
-rc=$?; cp /tmp/prod_keep.so $L/libfa_mi355x.so; tail -3 gpurun_out/pytest_rsa.log; [ $rc -eq 0 ] || exit $rc
-VARS="rsa" OUT=rsa2 bash flash-attention-cuda_amd/tools/ab_vars.sh > gpurun_out/rsa2.txt 2>&1 || exit 1
-AB="timeout -k 10 300 python flash-attention-cuda_amd/tools/ab.py --configs auto --libs prod,rsa --head-dim 64"
-O=gpurun_out/ab_rsa2_d64.jsonl
-$AB --seq 8192 --causal --rounds 5 --iters 20 > $O &&
-$AB --seq 4096 --batch 64 --causal --rounds 5 --iters 10 >> $O || exit 1
-grep -v amdgpu.ids gpurun_out/rsa2.txt
-python - $O <<'PY'
-import json, sys
-for l in open(sys.argv[1]):
-    r = json.loads(l)
-    print(f'd64 {r["lib"]:>8} B={r["batch"]:<3} S={r["seq"]:<6} {"c " if r["causal"] else "nc"} {r["median_tflops"]:8.1f}')
+for i in 1 2 3; do
+  timeout -k 10 300 python bench.py --no-sweep --no-cpu-baseline --no-pmc 2>/dev/null | tail -1 || exit 1
+done > gpurun_out/bench_repeat.jsonl
+python - <<'PY'
+import json
+for l in open("gpurun_out/bench_repeat.jsonl"):
+    d = json.loads(l); print(d["value"], d["ms_per_step"])
 PY
