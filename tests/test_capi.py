@@ -359,3 +359,26 @@ def test_generated_item_program_is_current(tmp_path):
     with open(os.path.join(csrc, "fa_w4_item.inc")) as f:
         committed = f.read()
     assert out.read_text() == committed, "fa_w4_item.inc is stale: run `make -C flash-attention-cuda_amd`"
+
+
+@pytest.mark.parametrize("env", [
+    {"W4_XP": "rsa"}, {"W4_XP": "cvtearly"}, {"W4_XP": "kpre"}, {"W4_XP": "shift4"},
+    {"W4_XP": "nomfz"}, {"W4_WAGE": "0"}, {"W4_V_AHEAD": "5"}, {"W4_DIAG": "stamps"},
+    {"W4_DIAG": "prostamps"},
+], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+def test_generator_variants_generate(tmp_path, env):
+    """The experiment / diagnostic switches DESIGN.md cites (tools/w4_variant.sh
+    builds) still generate a complete item program: every filler lands in an
+    MFMA gap and every function is emitted."""
+    import sys
+
+    csrc = os.path.join(ROOT, "flash-attention-cuda_amd", "csrc")
+    out = tmp_path / "fa_w4_item.inc"
+    e = {k: v for k, v in os.environ.items() if not k.startswith("W4_")}
+    e.update(env)
+    subprocess.run([sys.executable, os.path.join(csrc, "gen_w4_item.py"), str(out)], check=True,
+                   env=e, timeout=300)
+    text = out.read_text()
+    for fn in ("w4_item_noncausal_f16", "w4_item_causal_bf16", "w4_item_causal_split_f16",
+               "w4_item_causal_d64_f16"):
+        assert f"void {fn}(" in text, fn
