@@ -527,6 +527,11 @@ CVT_EARLY = "cvtearly" in XP
 # the 8 row-sum MFMAs of PV(j) at the start of phase A(j+1), under the K
 # reads' latency, instead of at the end of the exp2-bound phase B(j)
 RSA = "rsa" in XP
+# head_dim 128: V(0) / K(1) written before the prologue's first barrier with
+# K(0), one barrier per item seam instead of two (+0.3-0.8 %; at 64 level to
+# -0.5 %, profiles/r04_ab_w4_one_barrier_seam{,_d64}.jsonl; W4_XP=twobar
+# keeps two at 128 too)
+ONEBAR_XP = "twobar" not in XP
 # gap of a chain's maxima within chain x + LAG, and the first phase-B gap of
 # phase A's leftover maxima: one gap later than the hazard windows need
 # spares 3 of a tile's 5 s_nop (profiles/r04_ab_w4_nop_trim*.jsonl)
@@ -1427,6 +1432,14 @@ def prologue(st, causal, split=False):
     for i in range(NPASS()):
         st.raw(f"ds_write_b128 %[klds], {R('v', 112 + 4 * i, 4)} offset:{KBUF[0] + PASSL() * i}")
     q_scale(st)
+    if ONEBAR_XP and HDC["hd"] == 128:
+        # V(0), K(1) (prefetched after Q, K(0)) landed under the Q scaling:
+        # into their LDS images before the same barrier as K(0) -- the
+        # previous item's last barrier freed every image
+        st.raw(f"s_waitcnt vmcnt({sg0()})")
+        for i in range(NPASS()):
+            st.raw(f"ds_write_b128 %[vlds], {vst(i, 1)} offset:{VBUF[0] + PASSL() * i}")
+            st.raw(f"ds_write_b128 %[klds], {kst(i, 1)} offset:{KBUF[1] + PASSL() * i}")
     prostamp(st, 1)  # -> K(0) written, Q scaled
     st.raw("s_waitcnt lgkmcnt(0)")
     st.raw("s_barrier")
@@ -1457,7 +1470,9 @@ def prologue(st, causal, split=False):
     prostamp(st, 3)  # -> first softmax + exp2 done
     # V(0), K(1) landed: into their LDS images (warm with the deferred
     # epilogue: its 16 O stores are the youngest, behind stage 0's 8 loads)
-    if xovl:
+    if ONEBAR_XP and HDC["hd"] == 128:
+        pass
+    elif xovl:
         cw, cd = newlabel("coldw"), newlabel("waitdone")
         st.raw(f"s_cmp_eq_u32 {WARM}, 0")
         st.branch("s_cbranch_scc1", cw)
@@ -1468,12 +1483,13 @@ def prologue(st, causal, split=False):
         st.label(cd)
     else:
         st.raw(f"s_waitcnt vmcnt({sg0()})")
-    for i in range(NPASS()):
-        st.raw(f"ds_write_b128 %[vlds], {vst(i, 1)} offset:{VBUF[0] + PASSL() * i}")
-        st.raw(f"ds_write_b128 %[klds], {kst(i, 1)} offset:{KBUF[1] + PASSL() * i}")
-    st.raw("s_waitcnt lgkmcnt(0)")
-    st.lgkm = []
-    st.raw("s_barrier")
+    if not (ONEBAR_XP and HDC["hd"] == 128):
+        for i in range(NPASS()):
+            st.raw(f"ds_write_b128 %[vlds], {vst(i, 1)} offset:{VBUF[0] + PASSL() * i}")
+            st.raw(f"ds_write_b128 %[klds], {kst(i, 1)} offset:{KBUF[1] + PASSL() * i}")
+        st.raw("s_waitcnt lgkmcnt(0)")
+        st.lgkm = []
+        st.raw("s_barrier")
     prostamp(st, 4)  # -> V(0), K(1) written, loop start
     pstamp(st, 62)
     if RSA:
