@@ -257,6 +257,8 @@ __global__ __launch_bounds__(WAVES * 64, 2) void fa_fwd_f16_persistent_kernel(
 
 // one wave per SIMD, 64 query rows per wave, asm-owned register file
 #include "fa_w4_kernel.hpp"
+// one wave per SIMD, 16 rows of each of two query blocks per wave (short sequences)
+#include "fa_w4p_kernel.hpp"
 
 namespace fa {
 
@@ -340,7 +342,8 @@ struct Config {
   fa_config_info_t info;
   int sched;  // 0 = one barrier per tile, 1 = 8-wave ping-pong, 3 = ping-pong + LDS-DMA tiles
   int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent, 3 = KV-pair,
-              // 4 = KV-quad, 5 = persistent, one wave per SIMD (W4, asm item program)
+              // 4 = KV-quad, 5 = persistent, one wave per SIMD (W4, asm item program),
+              // 6 = paired 64-row query blocks, one wave per SIMD (W4P, asm item program)
   kernel_fn fn;
 };
 
@@ -348,6 +351,8 @@ template <int W, int BN_, int C, int KIND, int SCHED, int DT, int HDIM>
 constexpr kernel_fn pick_kernel() {
   if constexpr (KIND == 5)
     return fa_fwd_f16_w4_kernel<(C != 0), DT == 1, HDIM>;
+  else if constexpr (KIND == 6)
+    return fa_fwd_w4p_kernel<(C != 0), DT == 1>;
 
   else if constexpr (KIND == 3)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
@@ -388,6 +393,10 @@ constexpr kernel_fn pick_kernel() {
   {{ID, 256, 64, 4, C, 0, kW4LdsBytes, NAME, DT, HDIM}, 0, 5,                            \
    pick_kernel<4, 64, C, 5, 0, DT, HDIM>()}
 #define FA_CFG_W4(ID, C, DT, NAME) FA_CFG_W4D(ID, C, DT, 128, NAME)
+// W4P: 4 waves x (16 + 16) query rows of two 64-row blocks, K/V double-buffered (64 KB)
+#define FA_CFG_W4P(ID, C, DT, NAME)                                                    \
+  {{ID, 128, 64, 4, C, 0, kW4PLdsBytes, NAME, DT, 128}, 0, 6,                            \
+   pick_kernel<4, 64, C, 6, 0, DT, 128>()}
 
 // Only tiers the dispatcher picks, explicit entry points (split-KV) and the
 // baselines a test compares against (the per-item ping-pong 2/3: the
@@ -448,6 +457,11 @@ static const Config kConfigs[] = {
     FA_CFG_W4D(45, 1, 0, 64, "d64_bm256_bn64_w4x64_m16_asm_persistent_causal"),
     FA_CFG_W4D(46, 0, 1, 64, "bf16_d64_bm256_bn64_w4x64_m16_asm_persistent_noncausal"),
     FA_CFG_W4D(47, 1, 1, 64, "bf16_d64_bm256_bn64_w4x64_m16_asm_persistent_causal"),
+    // paired 64-row query blocks, one wave per SIMD, asm item program (fa_w4p_kernel.hpp)
+    FA_CFG_W4P(48, 0, 0, "bm128_bn64_w4x32_m16_asm_pair_noncausal"),
+    FA_CFG_W4P(49, 1, 0, "bm128_bn64_w4x32_m16_asm_pair_causal"),
+    FA_CFG_W4P(50, 0, 1, "bf16_bm128_bn64_w4x32_m16_asm_pair_noncausal"),
+    FA_CFG_W4P(51, 1, 1, "bf16_bm128_bn64_w4x32_m16_asm_pair_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 

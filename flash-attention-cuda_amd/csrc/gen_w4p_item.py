@@ -1,0 +1,787 @@
+#!/usr/bin/env python3
+"""Generator of the paired one-wave-per-SIMD item program (fa_w4p_item.inc).
+
+The short-sequence tier W4P (fa_w4p_kernel.hpp): one workgroup = 4 waves, one
+per SIMD, on TWO 64-row query blocks of one head, X0 and X1.  Wave w holds 16
+rows of each -- row block 0 = rows 64 X0 + 16 w + r16, row block 1 = rows
+64 X1 + 16 w + r16 -- and the four waves walk ONE shared K/V stream (key
+tiles 0 .. T0-1, double-buffered LDS images filled by LDS-DMA, exactly the
+W4 images).  Causal launches pair a heavy block X0 = nqb-1-i with a light
+one X1 = i of the same head, so every workgroup costs nqb+1 key tiles of 64
+rows (the reference's heaviest-first order, flash_attention.cu:103-112,
+taken to its balanced end), and a launch of B*H*S/128 rows fills the chip at
+S = 1024 (B=1, H=32: 256 workgroups) where 256-row items (W4) leave half of
+it idle and the 128-row KV-pair's heaviest block is 8/4.5 of the mean.
+
+Per key tile j (after the prologue computed S(0)) a wave runs, with NB = the
+row blocks still active (2 while the light block lasts, then 1):
+  phase A: QK^T(j+1), 16 NB MFMAs in 4 NB four-deep chains, beside the fp16
+           conversion of P(j), the running maxima of S(j+1), the K fragment
+           reads (each feeds NB MFMAs) and the LDS-DMA of K(j+2) / V(j+1)
+  phase B: PV(j) + row sums, 18 NB MFMAs, beside the rescale decision and
+           exp2 of S(j+1) and the V^T transposed reads
+  s_waitcnt vmcnt(0), one barrier.
+Tiles that end a block (its causal diagonal or ragged last tile, its PV
+drain) run one generic iteration instead: conversions, QK^T, PV, then the
+limit mask, maxima, rescale decision and exp2, per active block.
+
+The arithmetic is M16's (fa_fwd_kernel.hpp) with the rescale decision per
+16-row block, checked against the oracle (reference cpu_attention) at the
+1e-3 gate.  Hazards and LDS waits: gen_w4_item.Stream.
+
+usage: python3 gen_w4p_item.py [OUT.inc]      (the Makefile runs it)
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import gen_w4_item as w4  # noqa: E402
+from gen_w4_item import DT, NINF, R, Stream, dsr, mfma, salu, set_dtype, valu, vmem  # noqa: E402
+
+NT, NE = 4, 8          # head_dim 128: k-steps of a QK^T chain, 16-column O blocks
+ROWB = 256             # bytes of a Q/K/V/O row
+TILEB = 64 * ROWB      # a 64-key K or V tile
+PASSL = 4096           # LDS stride of a staging pass
+RESCALE = "0x41000000"  # 8.0: m_ref moves when a row max grew past it (log2 units)
+
+# ---------------------------------------------------------------------------
+# register map (VGPR v0-v165, AGPR a0-a135; the compiler keeps the rest)
+# ---------------------------------------------------------------------------
+
+
+def S(b, cb, i=None):      # S^T tile: block b, 16-key block cb (fp32, exp2'd in place)
+    base = 16 * b + 4 * cb
+    return R("v", base, 4) if i is None else R("v", base + i)
+
+
+def P(b, u, r=None):       # P fp16, B operand of PV: block b, 32-key step u
+    base = 32 + 8 * b + 4 * u
+    return R("v", base, 4) if r is None else R("v", base + r)
+
+
+def NEGM(b, i=None):       # -m_ref broadcast: C operand of the first MFMA of a chain
+    return R("v", 48 + 4 * b, 4) if i is None else R("v", 48 + 4 * b + i)
+
+
+def KF(slot):              # K fragments: 8 slots (two 16-key blocks)
+    return R("v", 56 + 4 * slot, 4)
+
+
+def VF(slot, half=None):   # V^T fragments: 8 slots
+    base = 88 + 4 * slot
+    return R("v", base, 4) if half is None else R("v", base + 2 * half, 2)
+
+
+def KD(i):                 # per-pass LDS-DMA source offsets
+    return R("v", 120 + i)
+
+
+def VD(i):
+    return R("v", 124 + i)
+
+
+ONES = R("v", 128, 4)
+MREF = [R("v", 132), R("v", 133)]
+RMAX = [R("v", 134), R("v", 135)]            # running partial maxima per block
+VNINF = R("v", 136)
+T = [R("v", 137 + i) for i in range(11)]     # v137-v147 temporaries
+KOFF = ["%[koff]"] + [R("v", 148 + i) for i in range(3)]
+VOFF = ["%[voff]"] + [R("v", 151 + i) for i in range(3)]
+EPI = [f"v{154 + i}" for i in range(8)]      # epilogue staging
+XY = ["v162", "v163", "v164", "v165"]        # one store: X = v162,163 ; Y = v164,165
+NV = 166
+
+
+def O(b, e, i=None):       # O^T accumulator, block b, d-block e
+    base = 32 * b + 4 * e
+    return R("a", base, 4) if i is None else R("a", base + i)
+
+
+def L(b, i=None):          # row sums l
+    return R("a", 64 + 4 * b, 4) if i is None else R("a", 64 + 4 * b + i)
+
+
+def Q(b, t):               # Q * c (fp16), B operand of QK^T
+    return R("a", 72 + 16 * b + 4 * t, 4)
+
+
+def KST1(i):               # prologue staging: K(1) / V(0)
+    return R("a", 104 + 4 * i, 4)
+
+
+def VST1(i):
+    return R("a", 120 + 4 * i, 4)
+
+
+NA = 136
+
+# LDS images (W4's): K at 0 / 16384, V at 32768 / 49152
+KBUF = [0, 16384]
+VBUF = [32768, 49152]
+KADDR = [f"%[ka{t}]" for t in range(4)]
+VADDR = ["%[va0]", "%[va1]"]
+
+# SGPR scratch (clobbered s40-s71)
+SK, SV = "s[40:43]", "s[44:47]"
+SKREM, SVREM = "s48", "s49"
+SJ, SJ1 = "s50", "s51"
+ST0, ST1 = "s52", "s53"
+KV0 = "s54"
+RQ, RO = "s[56:59]", "s[60:63]"
+SM0 = "s64"
+DIVS = "s[66:67]"
+NS_LO, NS_HI = 40, 72
+
+# block b's row base (64 X_b + 16 w), key bound, of the C++ side
+QR = ["%[qr0]", "%[qr1]"]
+KVH = ["%[kvh0]", "%[kvh1]"]
+
+MAX_OFF, LEFT_OFF, DEC_GAP = 2, 3, 6
+LAG = 2
+
+
+def vahead(nb):
+    """V^T fragments read ahead of their PV MFMAs: 8 (nb = 2) / 6 (nb = 1)
+    MFMAs of cover for the LDS latency"""
+    return 4 if nb == 2 else 6
+
+
+def kslot(cb, t):
+    return 4 * (cb & 1) + t
+
+
+def k_read(t, cb, kb):
+    s = kslot(cb, t)
+    return dsr(f"ds_read_b128 {KF(s)}, {KADDR[t]} offset:{kb + 4096 * cb}", KF(s), KADDR[t])
+
+
+def v_reads(f, vb):
+    u, e = divmod(f, NE)
+    slot = f % 8
+    off = vb + 8192 * u + 512 * (e >> 1)
+    a = VADDR[e & 1]
+    return [dsr(f"ds_read_b64_tr_b16 {VF(slot, 0)}, {a} offset:{off}", VF(slot, 0), a),
+            dsr(f"ds_read_b64_tr_b16 {VF(slot, 1)}, {a} offset:{off + 4096}", VF(slot, 1), a)]
+
+
+def qk_chain(b, cb):
+    out = []
+    for t in range(NT):
+        c = NEGM(b) if t == 0 else S(b, cb)
+        out.append(mfma(S(b, cb), KF(kslot(cb, t)), Q(b, t), c))
+    return out
+
+
+def cvt_block(b, cb):
+    p = 32 + 8 * b + 4 * (cb >> 1) + 2 * (cb & 1)
+    s = 16 * b + 4 * cb
+    return [valu(f"{DT['cvt_pk']} v{p}, v{s}, v{s + 1}", r=[f"v{s}", f"v{s + 1}"], w=[f"v{p}"]),
+            valu(f"{DT['cvt_pk']} v{p + 1}, v{s + 2}, v{s + 3}", r=[f"v{s + 2}", f"v{s + 3}"], w=[f"v{p + 1}"])]
+
+
+def max_block(b, cb, first):
+    s = 16 * b + 4 * cb
+    m = RMAX[b]
+    if first:
+        return [valu(f"v_max3_f32 {m}, v{s}, v{s + 1}, v{s + 2}", r=[f"v{s}", f"v{s + 1}", f"v{s + 2}"], w=[m]),
+                valu(f"v_max_f32 {m}, {m}, v{s + 3}", r=[m, f"v{s + 3}"], w=[m])]
+    return [valu(f"v_max3_f32 {m}, {m}, v{s}, v{s + 1}", r=[m, f"v{s}", f"v{s + 1}"], w=[m]),
+            valu(f"v_max3_f32 {m}, {m}, v{s + 2}, v{s + 3}", r=[m, f"v{s + 2}", f"v{s + 3}"], w=[m])]
+
+
+def exp_ops(b):
+    return [valu(f"v_exp_f32 v{x}, v{x}", r=[f"v{x}"], w=[f"v{x}"], kind="trans")
+            for x in range(16 * b, 16 * b + 16)]
+
+
+def pv_mfmas(nb):
+    """PV + row sums: for u: for e: nb blocks; then nb row sums"""
+    ms, frag_first = [], {}
+    for u in range(2):
+        for e in range(NE):
+            frag_first[u * NE + e] = len(ms)
+            for b in range(nb):
+                ms.append(mfma(O(b, e), VF((u * NE + e) % 8), P(b, u), O(b, e)))
+        ms += [mfma(L(b), ONES, P(b, u), L(b)) for b in range(nb)]
+    return ms, frag_first
+
+
+def dma_pieces(p):
+    """LDS-DMA of K(j+2) -> kbuf[p], V(j+1) -> vbuf[1-p]: (M0 set, load)
+    pairs, then the descriptors advance one tile (gen_w4_item.dma_loads)"""
+    pairs = []
+    for i in range(4):
+        pairs.append((salu(f"s_add_u32 m0, %[dmab], {KBUF[p] + 1024 * i}"),
+                      vmem(f"buffer_load_dwordx4 {KD(i)}, {SK}, 0 offen lds", r=[KD(i)])))
+    for i in range(4):
+        pairs.append((salu(f"s_add_u32 m0, %[dmab], {VBUF[1 - p] + 1024 * i}"),
+                      vmem(f"buffer_load_dwordx4 {VD(i)}, {SV}, 0 offen lds", r=[VD(i)])))
+    adv = [[salu("s_add_u32 s40, s40, 0x4000"), salu("s_addc_u32 s41, s41, 0")],
+           [salu(f"s_sub_i32 {SKREM}, {SKREM}, 0x4000"), salu(f"s_max_i32 s42, {SKREM}, 0")],
+           [salu("s_add_u32 s44, s44, 0x4000"), salu("s_addc_u32 s45, s45, 0")],
+           [salu(f"s_sub_i32 {SVREM}, {SVREM}, 0x4000"), salu(f"s_max_i32 s46, {SVREM}, 0")]]
+    return pairs, adv
+
+
+# ---------------------------------------------------------------------------
+# the steady iteration: phase A / phase B interleaved
+# ---------------------------------------------------------------------------
+def phase_a(st, p, nb):
+    """QK^T(j+1) of nb blocks from kbuf[1-p] beside cvt P(j), maxima of S(j+1),
+    K reads, the stage's LDS-DMA and the first V^T fragments of PV(j)"""
+    kb = KBUF[1 - p]
+    chains = [(b, cb) for cb in range(4) for b in range(nb)]
+    mf = []
+    for b, cb in chains:
+        mf += qk_chain(b, cb)
+    n = len(mf)
+    gaps = {}
+
+    def put(k, ins):
+        gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
+
+    put(0, [k_read(t, 0, kb) for t in range(NT)])
+    for x, (b, cb) in enumerate(chains):
+        c = cvt_block(b, cb)
+        if cb == 0:
+            put(0, c)
+        else:
+            put(NT * x - 1, c[0])
+            put(NT * x, c[1])
+        if b == 0 and cb < 3:
+            for t in range(NT):
+                put(NT * x + 1 + t % 3, k_read(t, cb + 1, kb))
+        if x >= LAG:
+            by, cby = chains[x - LAG]
+            mm = max_block(by, cby, first=(cby == 0))
+            put(NT * x + MAX_OFF, mm[0])
+            put(min(NT * x + MAX_OFF + 1, n), mm[1])
+    # LDS-DMA: an M0 write and its load are always an MFMA apart (M0 wait
+    # state); nb = 2 spreads them over two gaps each, nb = 1 shares gaps
+    pairs, adv = dma_pieces(p)
+    a0, sp = (2, 2) if nb == 2 else (1, 1)
+    for i, (m0, ld) in enumerate(pairs):
+        put(a0 + sp * i, m0)
+        put(a0 + sp * i + 1, ld)
+    g = a0 + sp * (len(pairs) - 1) + 2
+    for i, ins in enumerate(adv):
+        put(g + i, ins)
+    # the first V^T fragments of PV(j) (V(j) is ready since the last barrier)
+    va = vahead(nb)
+    for f in range(va):
+        for i, r in enumerate(v_reads(f, VBUF[p])):
+            put(n - 2 * va + 2 * f + i, r)
+    assert max(gaps) <= n, "every filler lands in a gap"
+    st.interleave(mf, gaps)
+    left = []
+    for y in range(len(chains) - LAG, len(chains)):
+        by, cby = chains[y]
+        left += max_block(by, cby, first=False)
+    return left
+
+
+def slow_softmax(st, blocks, first):
+    """rescale (the M16 softmax's rare branch) per 16-row block: m_ref moves
+    when a lane's partial max of the block grew past RESCALE.  first: the
+    item's first tile -- every row centres on its max (a fully masked row,
+    max -inf, keeps m_ref = 0)."""
+    for b in blocks:
+        skip = w4.newlabel("pskip")
+        if not first:
+            st.emit(valu(f"v_cmp_lt_f32 vcc, {RESCALE}, {RMAX[b]}", r=[RMAX[b]]))
+            st.branch("s_cbranch_vccz", skip)
+        mx, sh = T[1], T[2]
+        row_max_b(st, b, mx)
+        if first:
+            st.emit(valu(f"v_cmp_eq_f32 vcc, {VNINF}, {mx}", r=[VNINF, mx]))
+            st.emit(valu(f"v_cndmask_b32_e64 {sh}, {mx}, 0, vcc", r=[mx], w=[sh]))
+        else:
+            st.emit(valu(f"v_max_f32 {sh}, 0, {mx}", r=[mx], w=[sh]))
+        shift_block(st, b, sh, first)
+        if not first:
+            st.label(skip)
+
+
+def row_max_b(st, b, dst):
+    s = [f"v{16 * b + i}" for i in range(16)]
+    st.emit(valu(f"v_max3_f32 {dst}, {s[0]}, {s[1]}, {s[2]}", r=s[0:3], w=[dst]))
+    for i in range(3, 15, 2):
+        st.emit(valu(f"v_max3_f32 {dst}, {dst}, {s[i]}, {s[i + 1]}", r=[dst, s[i], s[i + 1]], w=[dst]))
+    st.emit(valu(f"v_max_f32 {dst}, {dst}, {s[15]}", r=[dst, s[15]], w=[dst]))
+    tmp = T[10]
+    for sw in ("v_permlane16_swap_b32", "v_permlane32_swap_b32"):
+        st.emit(valu(f"v_mov_b32 {tmp}, {dst}", r=[dst], w=[tmp]))
+        st.emit(valu(f"{sw} {dst}, {tmp}", r=[dst, tmp], w=[dst, tmp]))
+        st.emit(valu(f"v_max_f32 {dst}, {dst}, {tmp}", r=[dst, tmp], w=[dst]))
+
+
+def shift_block(st, b, sh, first):
+    """m_ref moves by sh: S -= sh, m_ref += sh, negm = -m_ref; O, l *= 2^-sh"""
+    if not first:
+        alpha = T[3]
+        st.emit(valu(f"v_exp_f32 {alpha}, -{sh}", r=[sh], w=[alpha], kind="trans"))
+        regs = [O(b, e, i) for e in range(NE) for i in range(4)] + [L(b, i) for i in range(4)]
+        for a in regs:
+            st.emit(valu(f"v_accvgpr_read_b32 {T[4]}, {a}", r=[a], w=[T[4]]))
+            st.emit(valu(f"v_mul_f32 {T[4]}, {T[4]}, {alpha}", r=[T[4], alpha], w=[T[4]]))
+            st.emit(valu(f"v_accvgpr_write_b32 {a}, {T[4]}", r=[T[4]], w=[a]))
+    for i in range(16):
+        x = f"v{16 * b + i}"
+        st.emit(valu(f"v_sub_f32 {x}, {x}, {sh}", r=[x, sh], w=[x]))
+    st.emit(valu(f"v_add_f32 {MREF[b]}, {MREF[b]}, {sh}", r=[MREF[b], sh], w=[MREF[b]]))
+    for i in range(4):
+        st.emit(valu(f"v_xor_b32 {NEGM(b, i)}, 0x80000000, {MREF[b]}", r=[MREF[b]], w=[NEGM(b, i)]))
+
+
+def phase_b(st, p, nb, leftover, label_slow, label_end):
+    """PV(j) of nb blocks from vbuf[p]; the rescale decision at DEC_GAP; exp2
+    of S(j+1) after it"""
+    vb = VBUF[p]
+    mf, frag_first = pv_mfmas(nb)
+    n = len(mf)
+    gaps = {}
+
+    def put(k, ins):
+        gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
+
+    va = vahead(nb)
+    for f in range(va, 2 * NE):
+        k = frag_first[f - va]
+        r = v_reads(f, vb)
+        put(k + 1, r[0])
+        put(k + 2, r[1])
+    for i, ins in enumerate(leftover):
+        put(LEFT_OFF + i, ins)
+    assert LEFT_OFF + len(leftover) - 1 <= DEC_GAP
+    if nb == 2:
+        dec = [valu(f"v_max_f32 {T[0]}, {RMAX[0]}, {RMAX[1]}", r=RMAX, w=[T[0]]),
+               valu(f"v_cmp_lt_f32 vcc, {RESCALE}, {T[0]}", r=[T[0]])]
+    else:
+        dec = [valu(f"v_cmp_lt_f32 vcc, {RESCALE}, {RMAX[0]}", r=[RMAX[0]])]
+    ex = [e for b in range(nb) for e in exp_ops(b)]
+    n_g = n - DEC_GAP
+    for i, e in enumerate(ex):
+        put(DEC_GAP + 1 + (i * n_g) // len(ex), e)
+    for k in range(DEC_GAP):
+        for f in gaps.get(k, []):
+            st.emit(f)
+        st.emit(mf[k])
+    for f in gaps.get(DEC_GAP, []):
+        st.emit(f)
+    for d in dec:
+        st.emit(d)
+    st.branch("s_cbranch_vccnz", label_slow)
+    for k in range(DEC_GAP, n):
+        if k > DEC_GAP:
+            for f in gaps.get(k, []):
+                st.emit(f)
+        st.emit(mf[k])
+    for f in gaps.get(n, []):
+        st.emit(f)
+    st.branch("s_branch", label_end)
+    # slow path: the remaining PV MFMAs (their V reads, no exps), then rescale
+    st.label(label_slow)
+    for k in range(DEC_GAP, n):
+        if k > DEC_GAP:
+            for f in gaps.get(k, []):
+                if isinstance(f, str) or f.kind != "trans":
+                    st.emit(f)
+        st.emit(mf[k])
+    for f in gaps.get(n, []):
+        if isinstance(f, str) or f.kind != "trans":
+            st.emit(f)
+    slow_softmax(st, range(nb), first=False)
+    for e in ex:
+        st.emit(e)
+    st.branch("s_branch", label_end)
+
+
+# ---------------------------------------------------------------------------
+# the generic iteration (a block's masked last QK^T, its PV drain)
+# ---------------------------------------------------------------------------
+def mask_block(st, b, causal):
+    """S(b) = -inf where key >= kv_hi_b or (causal) key > query row, for the
+    tile at key KV0 (key kv = KV0 + 16cb + 4sg + i, row = qr_b + r16):
+    valid iff 16cb + i <= lim = min(kvh_b - KV0 - 1 - 4sg, qr_b - KV0 + r16 - 4sg).
+    A tile inside both bounds gets lim >= 63: a no-op."""
+    st.raw(f"s_sub_i32 {ST0}, {KVH[b]}, {KV0}")
+    st.raw(f"s_sub_i32 {ST0}, {ST0}, 1")
+    st.raw(f"s_sub_i32 {ST1}, {QR[b]}, {KV0}")
+    lim_rag, lim = T[5], T[7]
+    st.emit(valu(f"v_sub_u32 {T[6]}, %[vt], %[r16]", r=["%[vt]", "%[r16]"], w=[T[6]]))   # -4sg
+    st.emit(valu(f"v_add_u32 {lim_rag}, {ST0}, {T[6]}", r=[T[6]], w=[lim_rag]))
+    if causal:
+        st.emit(valu(f"v_add_u32 {lim}, {ST1}, %[vt]", r=["%[vt]"], w=[lim]))
+        st.emit(valu(f"v_min_i32 {lim}, {lim}, {lim_rag}", r=[lim, lim_rag], w=[lim]))
+    else:
+        lim = lim_rag
+    for cb in range(4):
+        for i in range(4):
+            x = S(b, cb, i)
+            st.emit(valu(f"v_cmp_le_i32 vcc, {16 * cb + i}, {lim}", r=[lim]))
+            st.emit(valu(f"v_cndmask_b32 {x}, {VNINF}, {x}, vcc", r=[VNINF, x], w=[x]))
+
+
+def full_max(st, b):
+    for cb in range(4):
+        for ins in max_block(b, cb, first=(cb == 0)):
+            st.emit(ins)
+
+
+def qk_plain(st, kb, blocks):
+    """QK^T of one tile for `blocks`, not interleaved: per 16-key block its
+    four K fragments, then the chains (the next block's reads ahead)"""
+    for t in range(NT):
+        st.emit(k_read(t, 0, kb))
+    for cb in range(4):
+        if cb < 3:
+            for t in range(NT):
+                st.emit(k_read(t, cb + 1, kb))
+        for b in blocks:
+            for m in qk_chain(b, cb):
+                st.emit(m)
+
+
+def pv_plain(st, vb, blocks):
+    mf, frag_first = pv_mfmas(len(blocks))
+    assert list(blocks) == list(range(len(blocks)))
+    gaps = {}
+    va = 6
+    for f in range(2 * NE):
+        k = 0 if f < va else frag_first[f - va] + 1
+        for i, r in enumerate(v_reads(f, vb)):
+            gaps.setdefault(k if f < va else k + i, []).append(r)
+    st.interleave(mf, gaps)
+
+
+def dma_plain(st, p):
+    pairs, adv = dma_pieces(p)
+    for m0, ld in pairs:
+        st.emit(m0)
+        st.nop(1)
+        st.emit(ld)
+    for two in adv:
+        for ins in two:
+            st.emit(ins)
+
+
+def generic(st, p, causal):
+    """iteration j with a block boundary: P(j) of the blocks with a PV(j),
+    QK^T(j+1) of the blocks with a key tile j+1 (none: the drain), PV(j),
+    then the mask / maxima / rescale decision / exp2 of S(j+1) per block"""
+    kb, vb = KBUF[1 - p], VBUF[p]
+    nocvt1, noqk, qk1, qkdone = (w4.newlabel(x) for x in ("gnocvt1", "gnoqk", "gqk1", "gqkdone"))
+    pv1, pvdone, gend = (w4.newlabel(x) for x in ("gpv1", "gpvdone", "gend"))
+    for cb in range(4):
+        for c in cvt_block(0, cb):
+            st.emit(c)
+    st.raw(f"s_cmp_lt_u32 {SJ}, %[tl]")
+    st.branch("s_cbranch_scc0", nocvt1)
+    for cb in range(4):
+        for c in cvt_block(1, cb):
+            st.emit(c)
+    st.label(nocvt1)
+    st.raw(f"s_cmp_lt_u32 {SJ1}, %[th]")
+    st.branch("s_cbranch_scc0", noqk)
+    dma_plain(st, p)
+    st.raw(f"s_cmp_lt_u32 {SJ1}, %[tl]")
+    st.branch("s_cbranch_scc0", qk1)
+    qk_plain(st, kb, [0, 1])
+    st.branch("s_branch", qkdone)
+    st.label(qk1)
+    qk_plain(st, kb, [0])
+    st.label(qkdone)
+    st.label(noqk)
+    st.raw(f"s_cmp_lt_u32 {SJ}, %[tl]")
+    st.branch("s_cbranch_scc0", pv1)
+    pv_plain(st, vb, [0, 1])
+    st.branch("s_branch", pvdone)
+    st.label(pv1)
+    pv_plain(st, vb, [0])
+    st.label(pvdone)
+    # softmax of S(j+1), block 0 then (if it has the tile) block 1
+    st.raw(f"s_cmp_lt_u32 {SJ1}, %[th]")
+    st.branch("s_cbranch_scc0", gend)
+    st.raw(f"s_lshl_b32 {KV0}, {SJ1}, 6")
+    for b in range(2):
+        if b == 1:
+            st.raw(f"s_cmp_lt_u32 {SJ1}, %[tl]")
+            st.branch("s_cbranch_scc0", gend)
+        mask_block(st, b, causal)
+        full_max(st, b)
+        slow_softmax(st, [b], first=False)
+        for e in exp_ops(b):
+            st.emit(e)
+    st.label(gend)
+
+
+# ---------------------------------------------------------------------------
+# prologue / epilogue
+# ---------------------------------------------------------------------------
+def rsrc(st, dst, lo, hi, records):
+    st.raw(f"s_mov_b32 s{dst}, {lo}")
+    st.raw(f"s_and_b32 s{dst + 1}, {hi}, 0xffff")
+    st.raw(f"s_mov_b32 s{dst + 2}, {records}")
+    st.raw(f"s_mov_b32 s{dst + 3}, 0x20000")
+
+
+def q_scale(st):
+    """Q * c (fp32 product rounded to fp16 once, M16::scale_q) from v0-31 into
+    a72-103, eight elements at a time in the (free) V^T fragment registers"""
+    for x0 in range(0, 32, 8):
+        xs = range(x0, x0 + 8)
+        lo = {x: f"v{88 + 3 * (x - x0)}" for x in xs}
+        hi = {x: f"v{89 + 3 * (x - x0)}" for x in xs}
+        pk = {x: f"v{90 + 3 * (x - x0)}" for x in xs}
+        if DT["bf16"]:
+            for x in xs:
+                st.raw(f"v_lshlrev_b32_e32 {lo[x]}, 16, v{x}")
+                st.raw(f"v_and_b32_e32 {hi[x]}, 0xffff0000, v{x}")
+            for x in xs:
+                st.raw(f"v_mul_f32_e32 {lo[x]}, %[c], {lo[x]}")
+                st.raw(f"v_mul_f32_e32 {hi[x]}, %[c], {hi[x]}")
+        else:
+            for x in xs:
+                st.raw(f"v_fma_mix_f32 {lo[x]}, v{x}, %[c], neg(0) op_sel_hi:[1,0,0]")
+                st.raw(f"v_fma_mix_f32 {hi[x]}, v{x}, %[c], neg(0) op_sel:[1,0,0] op_sel_hi:[1,0,0]")
+        for x in xs:
+            st.raw(f"{DT['cvt_pk']} {pk[x]}, {lo[x]}, {hi[x]}")
+        for x in xs:
+            st.raw(f"v_accvgpr_write_b32 a{72 + x}, {pk[x]}")
+
+
+def prologue(st, causal):
+    """descriptors, Q (both blocks) / K(0) / V(0) / K(1) loads, Q scaling,
+    S(0) = K(0) Q^T with the tile-0 mask and the first-tile softmax"""
+    st.raw(f"s_mov_b32 {SM0}, m0")
+    st.raw(f"v_mov_b32 {KD(0)}, %[kdma]")
+    st.raw(f"v_mov_b32 {VD(0)}, %[vdma]")
+    for i in range(1, 4):
+        st.raw(f"v_add_u32 {KD(i)}, {1024 * i}, %[kdma]")
+        st.raw(f"v_xor_b32 {KD(i)}, {64 * i}, {KD(i)}")
+        st.raw(f"v_add_u32 {VD(i)}, {2048 * (i >> 1) + 128 * (i & 1)}, %[vdma]")
+        if i >= 2:
+            st.raw(f"v_xor_b32 {VD(i)}, 32, {VD(i)}")
+        st.raw(f"v_add_u32 {KOFF[i]}, {4096 * i}, %[koff]")
+        st.raw(f"v_add_u32 {VOFF[i]}, {4096 * i}, %[voff]")
+    st.raw(f"v_mov_b32 {VNINF}, {NINF}")
+    for i in range(4):
+        st.raw(f"v_mov_b32 v{128 + i}, {DT['one2']}")
+    rsrc(st, 56, "%[qlo]", "%[qhi]", "%[qrec]")
+    rsrc(st, 40, "%[klo]", "%[khi]", "%[kvrec]")
+    rsrc(st, 44, "%[vlo]", "%[vhi]", "%[kvrec]")
+    rsrc(st, 60, "%[olo]", "%[ohi]", "%[qrec]")
+    # Q rows qr_b + r16, chunk g of k-step t: (qr_b << 8) + qoff + 64 t
+    for b in range(2):
+        st.raw(f"s_lshl_b32 {ST0}, {QR[b]}, 8")
+        st.raw(f"v_add_u32 {T[b]}, {ST0}, %[qoff]")
+    for i in range(4):
+        st.raw(f"v_add_u32 {T[4 + i]}, {hex(TILEB)}, {KOFF[i]}")
+    st.nop(5)  # SALU-written descriptors -> buffer loads
+    for b in range(2):
+        for t in range(NT):
+            st.raw(f"buffer_load_dwordx4 {R('v', 16 * b + 4 * t, 4)}, {T[b]}, {RQ}, 0 offen offset:{64 * t}")
+    for i in range(4):
+        st.raw(f"buffer_load_dwordx4 {KF(i)}, {KOFF[i]}, {SK}, 0 offen")
+    for i in range(4):
+        st.raw(f"buffer_load_dwordx4 {VST1(i)}, {VOFF[i]}, {SV}, 0 offen")
+    for i in range(4):
+        st.raw(f"buffer_load_dwordx4 {KST1(i)}, {T[4 + i]}, {SK}, 0 offen")
+    # DMA descriptors start at K(2) / V(1)
+    t2, t1 = hex(2 * TILEB), hex(TILEB)
+    st.raw(f"s_add_u32 s40, s40, {t2}")
+    st.raw("s_addc_u32 s41, s41, 0")
+    st.raw(f"s_sub_i32 {SKREM}, s42, {t2}")
+    st.raw(f"s_max_i32 s42, {SKREM}, 0")
+    st.raw(f"s_add_u32 s44, s44, {t1}")
+    st.raw("s_addc_u32 s45, s45, 0")
+    st.raw(f"s_sub_i32 {SVREM}, s46, {t1}")
+    st.raw(f"s_max_i32 s46, {SVREM}, 0")
+    # O, l, -m_ref, m_ref = 0
+    for x in range(72):
+        st.raw(f"v_accvgpr_write_b32 a{x}, 0")
+    for x in range(48, 56):
+        st.raw(f"v_mov_b32 v{x}, 0")
+    for b in range(2):
+        st.raw(f"v_mov_b32 {MREF[b]}, 0")
+    # Q (8) and K(0) (4) landed; V(0), K(1) (8) may still fly
+    st.raw("s_waitcnt vmcnt(8)")
+    for i in range(4):
+        st.raw(f"ds_write_b128 %[klds], {KF(i)} offset:{KBUF[0] + PASSL * i}")
+    q_scale(st)
+    st.raw("s_waitcnt vmcnt(0)")
+    for i in range(4):
+        st.raw(f"ds_write_b128 %[vlds], {VST1(i)} offset:{VBUF[0] + PASSL * i}")
+        st.raw(f"ds_write_b128 %[klds], {KST1(i)} offset:{KBUF[1] + PASSL * i}")
+    st.raw("s_waitcnt lgkmcnt(0)")
+    st.raw("s_barrier")
+    st.nop(2)
+    # S(0): block 1 only if the item has one
+    one, s0done = w4.newlabel("s0one"), w4.newlabel("s0done")
+    st.raw("s_cmp_eq_u32 %[tl], 0")
+    st.branch("s_cbranch_scc1", one)
+    qk_plain(st, KBUF[0], [0, 1])
+    st.branch("s_branch", s0done)
+    st.label(one)
+    qk_plain(st, KBUF[0], [0])
+    st.label(s0done)
+    st.raw(f"s_mov_b32 {KV0}, 0")
+    blk1 = w4.newlabel("first1")
+    for b in range(2):
+        if b == 1:
+            st.raw("s_cmp_eq_u32 %[tl], 0")
+            st.branch("s_cbranch_scc1", blk1)
+        mask_block(st, b, causal)
+        slow_softmax(st, [b], first=True)
+        for e in exp_ops(b):
+            st.emit(e)
+    st.label(blk1)
+    # every wave's S(0) K reads are done before iteration 0's DMA refills kbuf[0]
+    st.lgkm_all()
+    st.raw("s_barrier")
+    st.raw(f"s_mov_b32 {SJ}, 0")
+
+
+def epilogue_block(st, b):
+    """O / l -> fp16 rows qr_b + r16 (M16::store_o: permlane16 swaps, dwordx4
+    stores, sc1)"""
+    l, inv = T[0], T[1]
+    st.raw(f"s_lshl_b32 {ST1}, {QR[b]}, 8")
+    st.emit(valu(f"v_accvgpr_read_b32 {l}, {L(b, 0)}", r=[L(b, 0)], w=[l]))
+    # inv = l > 0 ? 1.0f / l : 0  (IEEE division, the compiler's sequence)
+    st.emit(valu(f"v_div_scale_f32 {T[2]}, {DIVS}, {l}, {l}, 1.0", r=[l], w=[T[2]]))
+    st.emit(valu(f"v_rcp_f32_e32 {T[3]}, {T[2]}", r=[T[2]], w=[T[3]], kind="trans"))
+    st.emit(valu(f"v_fma_f32 {T[4]}, -{T[2]}, {T[3]}, 1.0", r=[T[2], T[3]], w=[T[4]]))
+    st.emit(valu(f"v_fmac_f32_e32 {T[3]}, {T[4]}, {T[3]}", r=[T[3], T[4]], w=[T[3]]))
+    st.emit(valu(f"v_div_scale_f32 {T[4]}, vcc, 1.0, {l}, 1.0", r=[l], w=[T[4]]))
+    st.emit(valu(f"v_mul_f32_e32 {T[5]}, {T[4]}, {T[3]}", r=[T[4], T[3]], w=[T[5]]))
+    st.emit(valu(f"v_fma_f32 {T[6]}, -{T[2]}, {T[5]}, {T[4]}", r=[T[2], T[5], T[4]], w=[T[6]]))
+    st.emit(valu(f"v_fmac_f32_e32 {T[5]}, {T[6]}, {T[3]}", r=[T[5], T[6], T[3]], w=[T[5]]))
+    st.emit(valu(f"v_fma_f32 {T[2]}, -{T[2]}, {T[5]}, {T[4]}", r=[T[2], T[5], T[4]], w=[T[2]]))
+    st.emit(valu(f"v_div_fmas_f32 {T[2]}, {T[2]}, {T[3]}, {T[5]}", r=[T[2], T[3], T[5]], w=[T[2]]))
+    st.emit(valu(f"v_div_fixup_f32 {T[2]}, {T[2]}, {l}, 1.0", r=[T[2], l], w=[T[2]]))
+    st.emit(valu(f"v_cmp_lt_f32 vcc, 0, {l}", r=[l]))
+    st.emit(valu(f"v_cndmask_b32 {inv}, 0, {T[2]}, vcc", r=[T[2]], w=[inv]))
+    st.emit(valu(f"v_add_u32 {T[7]}, {ST1}, %[ooff]", r=["%[ooff]"], w=[T[7]]))
+    for ep in range(NE // 2):
+        for x in range(2):
+            e = 2 * ep + x
+            for i in range(4):
+                d = EPI[4 * x + i]
+                st.emit(valu(f"v_accvgpr_read_b32 {d}, {O(b, e, i)}", r=[O(b, e, i)], w=[d]))
+            for i in range(4):
+                d = EPI[4 * x + i]
+                st.emit(valu(f"v_mul_f32_e32 {d}, {d}, {inv}", r=[d, inv], w=[d]))
+        X, Y = XY[0:2], XY[2:4]
+        st.emit(valu(f"{DT['cvt_pk']} {X[0]}, {EPI[0]}, {EPI[1]}", r=EPI[0:2], w=[X[0]]))
+        st.emit(valu(f"{DT['cvt_pk']} {X[1]}, {EPI[2]}, {EPI[3]}", r=EPI[2:4], w=[X[1]]))
+        st.emit(valu(f"{DT['cvt_pk']} {Y[0]}, {EPI[4]}, {EPI[5]}", r=EPI[4:6], w=[Y[0]]))
+        st.emit(valu(f"{DT['cvt_pk']} {Y[1]}, {EPI[6]}, {EPI[7]}", r=EPI[6:8], w=[Y[1]]))
+        for dw in range(2):
+            st.emit(valu(f"v_permlane16_swap_b32 {X[dw]}, {Y[dw]}", r=[X[dw], Y[dw]], w=[X[dw], Y[dw]]))
+        st.emit(vmem(f"buffer_store_dwordx4 v[162:165], {T[7]}, {RO}, 0 offen offset:{64 * ep} sc1",
+                     r=["v[162:165]", T[7]]))
+    st.nop(2)
+
+
+# ---------------------------------------------------------------------------
+def body(st, p, causal, Lb):
+    """iteration j (parity p = j & 1): steady with both blocks, steady with
+    block 0 alone, or generic; then the stage's DMA wait and the barrier"""
+    st.label(Lb["loop"][p], drain_lgkm=True)
+    st.raw(f"s_add_u32 {SJ1}, {SJ}, 1")
+    st.raw(f"s_add_u32 {ST0}, {SJ}, 2")
+    st.raw(f"s_cmp_lt_u32 {ST0}, %[tl]")       # j+2 < T1: both blocks steady
+    st.branch("s_cbranch_scc1", Lb["s2"][p])
+    st.raw(f"s_cmp_lt_u32 {SJ}, %[tl]")         # block 1 still has PV(j)
+    st.branch("s_cbranch_scc1", Lb["gen"][p])
+    st.raw(f"s_cmp_lt_u32 {ST0}, %[th]")        # j+2 < T0: block 0 steady alone
+    st.branch("s_cbranch_scc1", Lb["s1"][p])
+    st.branch("s_branch", Lb["gen"][p])
+    st.label(Lb["s2"][p])
+    left = phase_a(st, p, 2)
+    phase_b(st, p, 2, left, Lb["slow2"][p], Lb["end"][p])
+    st.label(Lb["s1"][p])
+    left = phase_a(st, p, 1)
+    phase_b(st, p, 1, left, Lb["slow1"][p], Lb["end"][p])
+    st.label(Lb["gen"][p])
+    generic(st, p, causal)
+    st.label(Lb["end"][p], drain_lgkm=True)
+    st.raw("s_waitcnt vmcnt(0)")   # this iteration's LDS-DMA landed before the barrier publishes it
+    st.raw("s_barrier")
+    st.raw(f"s_add_u32 {SJ}, {SJ}, 1")
+    st.raw(f"s_cmp_lt_u32 {SJ}, %[th]")
+    if p == 0:
+        st.branch("s_cbranch_scc0", Lb["done"])
+    else:
+        st.branch("s_cbranch_scc1", Lb["loop"][0])
+
+
+def generate(causal):
+    st = Stream()
+    Lb = {k: [w4.newlabel(f"{k}{p}") for p in range(2)]
+          for k in ("loop", "s2", "s1", "gen", "slow2", "slow1", "end")}
+    Lb["done"] = w4.newlabel("done")
+    prologue(st, causal)
+    body(st, 0, causal, Lb)
+    body(st, 1, causal, Lb)
+    st.label(Lb["done"], drain_lgkm=True)
+    epilogue_block(st, 0)
+    nob1 = w4.newlabel("nob1")
+    st.raw("s_cmp_eq_u32 %[tl], 0")
+    st.branch("s_cbranch_scc1", nob1)
+    epilogue_block(st, 1)
+    st.label(nob1)
+    st.raw(f"s_mov_b32 m0, {SM0}")
+    return st.out
+
+
+HEADER = """// GENERATED by gen_w4p_item.py -- do not edit.
+// One paired item (two 64-row query blocks x all key tiles) of the W4P tier:
+// see the generator's docstring for the register map and the schedule.
+#pragma once
+"""
+
+
+def cxx(causal, bf16, lines):
+    body_ = "\n".join(f'      "{ln}\\n"' for ln in lines)
+    vclob = ", ".join(f'"v{i}"' for i in range(NV))
+    aclob = ", ".join(f'"a{i}"' for i in range(NA))
+    sclob = ", ".join(f'"s{i}"' for i in range(NS_LO, NS_HI))
+    name = ("w4p_item_causal" if causal else "w4p_item_noncausal") + ("_bf16" if bf16 else "_f16")
+    return f"""
+__device__ __forceinline__ void {name}(const W4PRun& rn, const W4Lane& ln) {{
+  asm volatile(
+{body_}
+      :
+      : [qlo] "s"(rn.qlo), [qhi] "s"(rn.qhi), [klo] "s"(rn.klo), [khi] "s"(rn.khi),
+        [vlo] "s"(rn.vlo), [vhi] "s"(rn.vhi), [olo] "s"(rn.olo), [ohi] "s"(rn.ohi),
+        [qrec] "s"(rn.qrec), [kvrec] "s"(rn.kvrec), [qr0] "s"(rn.qr0), [qr1] "s"(rn.qr1),
+        [kvh0] "s"(rn.kvh0), [kvh1] "s"(rn.kvh1), [th] "s"(rn.th), [tl] "s"(rn.tl),
+        [c] "s"(rn.c), [dmab] "s"(rn.dmab),
+        [ka0] "v"(ln.ka[0]), [ka1] "v"(ln.ka[1]), [ka2] "v"(ln.ka[2]), [ka3] "v"(ln.ka[3]),
+        [va0] "v"(ln.va[0]), [va1] "v"(ln.va[1]), [koff] "v"(ln.koff), [voff] "v"(ln.voff),
+        [klds] "v"(ln.klds), [vlds] "v"(ln.vlds), [vt] "v"(ln.vt), [r16] "v"(ln.r16),
+        [qoff] "v"(ln.qoff), [ooff] "v"(ln.ooff), [kdma] "v"(ln.kdma), [vdma] "v"(ln.vdma)
+      : "memory", "vcc", "scc", {sclob},
+        {vclob},
+        {aclob});
+}}
+"""
+
+
+def main():
+    out = sys.argv[1] if len(sys.argv) > 1 else "fa_w4p_item.inc"
+    text = HEADER
+    for bf16 in (False, True):
+        set_dtype(bf16)
+        for causal in (False, True):
+            w4._lbl[0] = 0
+            text += cxx(causal, bf16, generate(causal))
+    set_dtype(False)
+    with open(out, "w") as f:
+        f.write(text)
+
+
+if __name__ == "__main__":
+    main()

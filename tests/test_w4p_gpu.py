@@ -1,0 +1,148 @@
+"""Paired short-sequence tier (bm128_bn64_w4x32_m16_asm_pair_*, fa_w4p_kernel.hpp +
+the generated item program fa_w4p_item.inc).
+
+A workgroup holds two 64-row query blocks of one head (causal: the heavy
+block nqb-1-r with the light block r) on one shared K/V stream, 16 rows of
+each per wave.  Its rescale decision is per 16-row block (the 8-wave kernels
+take it per 32-row wave), so outputs are compared with the oracle (the
+reference's cpu_attention restatement) on sampled heads and with an fp32
+torch attention on every head, both at the 1e-3 gate; bf16 against the fp32
+torch reference at 5e-3 (no reference oracle exists for bf16).
+"""
+import math
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import oracle  # noqa: E402  (test infrastructure)
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-3
+PAIR = "bm128_bn64_w4x32_m16_asm_pair"
+
+
+def _fa():
+    import fa_mi355x
+
+    return fa_mi355x
+
+
+def _ids(prefix):
+    out = {c.causal: c.id for c in _fa().configs() if c.name in (f"{prefix}_noncausal", f"{prefix}_causal")}
+    assert set(out) == {False, True}, prefix
+    return out
+
+
+def _rand(shape, seed, scale=1.0, dtype=torch.float16):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    t = torch.empty(shape, dtype=torch.float32, device="cuda")
+    t.uniform_(-0.5 * scale, 0.5 * scale, generator=g)
+    return t.to(dtype)
+
+
+def _bits(t):
+    return t.detach().cpu().contiguous().view(torch.int16).numpy().view(np.uint16)
+
+
+def _torch_ref(q, k, v, causal):
+    """fp32 attention of the 16-bit inputs, head by head (bounded memory)"""
+    b, h, s, d = q.shape
+    out = torch.empty((b, h, s, d), dtype=torch.float32, device=q.device)
+    mask = torch.ones((s, s), dtype=torch.bool, device=q.device).tril() if causal else None
+    for bi in range(b):
+        for hi in range(h):
+            sc = (q[bi, hi].float() @ k[bi, hi].float().t()) / math.sqrt(d)
+            if causal:
+                sc = sc.masked_fill(~mask, float("-inf"))
+            out[bi, hi] = torch.softmax(sc, dim=-1) @ v[bi, hi].float()
+    return out
+
+
+def _check(b, h, s, causal, seed, scale=1.0, dtype=torch.float16, oracle_heads=True):
+    fa = _fa()
+    pre = PAIR if dtype == torch.float16 else "bf16_" + PAIR
+    q, k, v = (_rand((b, h, s, 128), seed + i, scale if i < 2 else 1.0, dtype) for i in range(3))
+    out = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(pre)[causal])
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all()
+    ref = _torch_ref(q, k, v, causal)
+    d = (out.float() - ref).abs().max().item()
+    tol = TOL if dtype == torch.float16 else 5e-3
+    assert d <= tol, f"max diff vs fp32 torch {d}"
+    if oracle_heads and dtype == torch.float16:
+        for flat in sorted({0, b * h // 2, b * h - 1}):
+            bi, hi = divmod(flat, h)
+            sl = (slice(bi, bi + 1), slice(hi, hi + 1))
+            ro = oracle.attention(*(_bits(x[sl]) for x in (q, k, v)), causal)
+            dd = oracle.max_abs_diff(_bits(out[sl]), ro)
+            assert dd <= TOL, f"head {flat}: max_diff vs oracle {dd}"
+    return d
+
+
+SHAPES = [
+    (1, 32, 1024),   # BASELINE config 1: 256 pairs, one per CU
+    (1, 8, 1000),    # ragged S: the last block 40 rows, its last tile 40 keys
+    (2, 3, 320),     # 5 query blocks (odd: the middle one unpaired), 6 heads (not % 8)
+    (1, 4, 64),      # one block per head: single-tile items
+    (1, 2, 65),      # two blocks, the second 1 row
+    (1, 1, 130),     # three blocks, one head
+    (1, 16, 2048),   # 512 pairs: two rounds of workgroups
+    (3, 40, 777),    # 120 heads, ragged
+    (1, 8, 256),     # 4 blocks: pairs (3, 0), (2, 1)
+    (4, 32, 512),
+]
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_pair_matches_oracle(shape, causal):
+    _check(*shape, causal, seed=700)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("s", [256, 1000, 2048])
+def test_pair_peaked_rescale(s, causal):
+    # Q, K x4: row maxima keep growing past the 2^8 threshold -> the slow paths
+    _check(1, 8, s, causal, seed=710, scale=4.0)
+
+
+def _random_shapes(n, seed):
+    rng = np.random.default_rng(seed)
+    return [(int(rng.integers(1, 3)), int(rng.integers(1, 41)), int(rng.integers(1, 2049)))
+            for _ in range(n)]
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", _random_shapes(6, 2027), ids=lambda s: "x".join(map(str, s)))
+def test_pair_random_shapes(shape, causal):
+    _check(*shape, causal, seed=720)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", [(1, 32, 1024), (1, 8, 1000), (2, 3, 320)], ids=lambda s: "x".join(map(str, s)))
+def test_pair_bf16(shape, causal):
+    _check(*shape, causal, seed=730, dtype=torch.bfloat16)
+
+
+def test_pair_causal_row0_and_ones():
+    """causal row 0 sees key 0 only: O[0] = V[0] exactly; V = 1 -> O = 1"""
+    fa = _fa()
+    q, k = (_rand((1, 4, 1024, 128), 740 + i) for i in range(2))
+    v = _rand((1, 4, 1024, 128), 742)
+    out = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(PAIR)[True])
+    assert torch.equal(out[:, :, 0], v[:, :, 0])
+    ones = torch.ones_like(v)
+    for causal in (False, True):
+        o1 = fa.flash_attention_fwd(q, k, ones, causal=causal, config=_ids(PAIR)[causal])
+        assert torch.equal(o1, ones)
+
+
+def test_pair_deterministic():
+    fa = _fa()
+    q, k, v = (_rand((1, 32, 1024, 128), 750 + i) for i in range(3))
+    a = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(PAIR)[True])
+    b = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(PAIR)[True])
+    assert torch.equal(a, b)
