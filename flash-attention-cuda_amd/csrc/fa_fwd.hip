@@ -601,7 +601,14 @@ static int launch_auto(int dtype, const void* q, const void* k, const void* v, v
 
 using namespace fa;
 
+// the tier table; pair = false skips the paired tier (it has no head_dim-64 twin)
+static int select_tier(int batch, int heads, int seq_len, int causal, bool pair);
+
 extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
+  return select_tier(batch, heads, seq_len, causal, true);
+}
+
+static int select_tier(int batch, int heads, int seq_len, int causal, bool pair) {
   // Tier table re-derived for 256 CUs (ref :620-661 picks by seq >= 2048 on
   // 58 SMs), from tools/small_s.py and tools/sweep.py on the box:
   //  * 8-wave persistent ping-pong (256 rows / workgroup) once there are
@@ -649,6 +656,18 @@ extern "C" int fa_select_config(int batch, int heads, int seq_len, int causal) {
     return cfg_for(256, 4, 64, c, 0, 5);
   }
   if (seq_len <= 256) return cfg_for(128, 4, 64, c, 0, 0);
+  // paired 64-row query blocks (W4P, fa_w4p_kernel.hpp): causal launches of
+  // at most two rounds of pairs on the device's CUs (every pair
+  // costs nqb64+1 key tiles; past two rounds the KV-pair's 8 waves win: B=4
+  // H=32 S=1024 709 vs 522), non-causal ones of one nearly full round (B=1
+  // H=32 S=1024 792 vs 670; at half a round the KV-quad/pair win: H=16 474
+  // vs 514); S <= 2048 (longer heads: measured against the KV-quad first)
+  // (profiles/r05_w4p_*ab*.jsonl)
+  if (pair) {
+    const long long nq64 = (seq_len + 63) / 64, pairs = bh * ((nq64 + 1) / 2), cus = num_cus();
+    if (nq64 <= 32 && (causal ? pairs <= 2 * cus : (4 * pairs >= 3 * cus && pairs <= cus)))
+      return cfg_for(128, 4, 64, c, 0, 6);
+  }
   // causal, two rounds of 64-row blocks over long heads (>= 32 blocks per
   // head): the KV-quad's four-way key split halves the heaviest block's key
   // loop against the KV-pair (B=1 H=4 S=8192 765 vs 599, H=2 S=16384 808 vs
@@ -668,7 +687,7 @@ static int launch_auto(int dtype, const void* q, const void* k, const void* v, v
   int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
   if (rc != FA_OK) return rc;
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
-  const int sel = fa_select_config(batch, heads, seq_len, causal);
+  const int sel = select_tier(batch, heads, seq_len, causal, head_dim == HD);
   // (head_dim 64 of the W4 tier is the same item program with 2-step QK^T
   // chains and register-staged K/V: +4-9 % over the 8-wave ping-pong at
   // head_dim 64, profiles/r04_ab_w4_d64.jsonl)

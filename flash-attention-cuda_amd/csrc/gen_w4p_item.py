@@ -21,9 +21,10 @@ row blocks still active (2 while the light block lasts, then 1):
   phase B: PV(j) + row sums, 18 NB MFMAs, beside the rescale decision and
            exp2 of S(j+1) and the V^T transposed reads
   s_waitcnt vmcnt(0), one barrier.
-Tiles that end a block (its causal diagonal or ragged last tile, its PV
-drain) run one generic iteration instead: conversions, QK^T, PV, then the
-limit mask, maxima, rescale decision and exp2, per active block.
+Tiles that end a block run their own interleaved kinds (KINDS): a block's
+last tile (causal diagonal or ragged end) takes QK^T without the running
+maxima, then the limit mask and the maxima, then PV with the decision ahead
+of its first MFMA; a block's PV drain runs beside the other block's QK^T.
 
 The arithmetic is M16's (fa_fwd_kernel.hpp) with the rescale decision per
 16-row block, checked against the oracle (reference cpu_attention) at the
@@ -139,6 +140,46 @@ KVH = ["%[kvh0]", "%[kvh1]"]
 MAX_OFF, LEFT_OFF, DEC_GAP = 2, 3, 6
 LAG = 2
 
+# diagnostic builds only (never the product library; tools/w4_variant.sh):
+# W4P_DIAG=stamps accumulates per wave the shader cycles of the prologue, of
+# each iteration kind (steady 2 blocks / steady 1 block / generic) with their
+# counts, of the end-of-iteration DMA wait + barrier and of the epilogue, and
+# stores them over O[qr0][0:16] (every lane the same 64 bytes)
+DIAG = os.environ.get("W4P_DIAG", "")
+STAMPS = DIAG == "stamps"
+# accumulators: s72 start, s74 path, s76 stamp, s78 s2, s79 s1, s80 gen,
+# s81 n_s2, s82 n_s1, s83 n_gen, s84 wait+barrier, s85 prologue, s86 epilogue
+# ("gen" = every iteration kind that ends a block: diagonal / ragged tile, drain)
+NS_DIAG = 88
+
+
+def stamp_now(st, dst):
+    if STAMPS:
+        st.raw(f"s_memtime s[{dst}:{dst + 1}]")
+        st.raw("s_waitcnt lgkmcnt(0)")
+        st.lgkm = []
+
+
+def stamp_path(st, k):
+    """at an iteration kind's label: its start stamp and id"""
+    if STAMPS:
+        stamp_now(st, 72)
+        st.raw(f"s_mov_b32 s74, {k}")
+
+
+def stamp_path_end(st):
+    """at the iteration end (before the DMA wait): the path's cycles and count"""
+    if not STAMPS:
+        return
+    stamp_now(st, 76)
+    st.raw("s_sub_u32 s75, s76, s72")
+    for k in range(3):
+        st.raw(f"s_cmp_eq_u32 s74, {k}")
+        st.raw("s_cselect_b32 s77, s75, 0")
+        st.raw("s_cselect_b32 s87, 1, 0")
+        st.raw(f"s_add_u32 s{78 + k}, s{78 + k}, s77")
+        st.raw(f"s_add_u32 s{81 + k}, s{81 + k}, s87")
+
 
 def vahead(nb):
     """V^T fragments read ahead of their PV MFMAs: 8 (nb = 2) / 6 (nb = 1)
@@ -194,15 +235,15 @@ def exp_ops(b):
             for x in range(16 * b, 16 * b + 16)]
 
 
-def pv_mfmas(nb):
-    """PV + row sums: for u: for e: nb blocks; then nb row sums"""
+def pv_mfmas(blocks):
+    """PV + row sums of `blocks`: for u: for e: the blocks; then their row sums"""
     ms, frag_first = [], {}
     for u in range(2):
         for e in range(NE):
             frag_first[u * NE + e] = len(ms)
-            for b in range(nb):
+            for b in blocks:
                 ms.append(mfma(O(b, e), VF((u * NE + e) % 8), P(b, u), O(b, e)))
-        ms += [mfma(L(b), ONES, P(b, u), L(b)) for b in range(nb)]
+        ms += [mfma(L(b), ONES, P(b, u), L(b)) for b in blocks]
     return ms, frag_first
 
 
@@ -226,11 +267,24 @@ def dma_pieces(p):
 # ---------------------------------------------------------------------------
 # the steady iteration: phase A / phase B interleaved
 # ---------------------------------------------------------------------------
-def phase_a(st, p, nb):
-    """QK^T(j+1) of nb blocks from kbuf[1-p] beside cvt P(j), maxima of S(j+1),
-    K reads, the stage's LDS-DMA and the first V^T fragments of PV(j)"""
+def phase_a(st, p, qk, cvt, pv, with_max=True, dma=True):
+    """QK^T(j+1) of the blocks `qk` from kbuf[1-p] beside the fp16 conversion
+    of P(j) of the blocks `cvt` (each just before the chain that overwrites
+    its scores), the maxima of S(j+1) (with_max), the K reads, the stage's
+    LDS-DMA and the first V^T fragments of PV(j) of the blocks `pv`.  No qk
+    (the drain): the conversions and V^T reads alone."""
     kb = KBUF[1 - p]
-    chains = [(b, cb) for cb in range(4) for b in range(nb)]
+    va = vahead(len(pv))
+    if not qk:
+        for b in cvt:
+            for cb in range(4):
+                for c in cvt_block(b, cb):
+                    st.emit(c)
+        for f in range(va):
+            for r in v_reads(f, VBUF[p]):
+                st.emit(r)
+        return []
+    chains = [(b, cb) for cb in range(4) for b in qk]
     mf = []
     for b, cb in chains:
         mf += qk_chain(b, cb)
@@ -242,41 +296,47 @@ def phase_a(st, p, nb):
 
     put(0, [k_read(t, 0, kb) for t in range(NT)])
     for x, (b, cb) in enumerate(chains):
-        c = cvt_block(b, cb)
-        if cb == 0:
-            put(0, c)
-        else:
-            put(NT * x - 1, c[0])
-            put(NT * x, c[1])
-        if b == 0 and cb < 3:
+        if b in cvt:
+            c = cvt_block(b, cb)
+            if cb == 0:
+                put(0, c)
+            else:
+                put(NT * x - 1, c[0])
+                put(NT * x, c[1])
+        if b == qk[0] and cb < 3:
             for t in range(NT):
                 put(NT * x + 1 + t % 3, k_read(t, cb + 1, kb))
-        if x >= LAG:
+        if with_max and x >= LAG:
             by, cby = chains[x - LAG]
             mm = max_block(by, cby, first=(cby == 0))
             put(NT * x + MAX_OFF, mm[0])
             put(min(NT * x + MAX_OFF + 1, n), mm[1])
-    # LDS-DMA: an M0 write and its load are always an MFMA apart (M0 wait
-    # state); nb = 2 spreads them over two gaps each, nb = 1 shares gaps
-    pairs, adv = dma_pieces(p)
-    a0, sp = (2, 2) if nb == 2 else (1, 1)
-    for i, (m0, ld) in enumerate(pairs):
-        put(a0 + sp * i, m0)
-        put(a0 + sp * i + 1, ld)
-    g = a0 + sp * (len(pairs) - 1) + 2
-    for i, ins in enumerate(adv):
-        put(g + i, ins)
+    # conversions of a block with a PV(j) but no QK(j+1) (its drain): any gap
+    extra = [c for b in cvt if b not in qk for cb in range(4) for c in cvt_block(b, cb)]
+    for i, c in enumerate(extra):
+        put(1 + (i * (n - 2)) // len(extra), c)
+    if dma:
+        # LDS-DMA: an M0 write and its load are always an MFMA apart (M0 wait
+        # state); two blocks spread them over two gaps each, one shares gaps
+        pairs, adv = dma_pieces(p)
+        a0, sp = (2, 2) if len(qk) == 2 else (1, 1)
+        for i, (m0, ld) in enumerate(pairs):
+            put(a0 + sp * i, m0)
+            put(a0 + sp * i + 1, ld)
+        g = a0 + sp * (len(pairs) - 1) + 2
+        for i, ins in enumerate(adv):
+            put(g + i, ins)
     # the first V^T fragments of PV(j) (V(j) is ready since the last barrier)
-    va = vahead(nb)
     for f in range(va):
         for i, r in enumerate(v_reads(f, VBUF[p])):
-            put(n - 2 * va + 2 * f + i, r)
+            put(max(0, n - 2 * va) + 2 * f + i, r)
     assert max(gaps) <= n, "every filler lands in a gap"
     st.interleave(mf, gaps)
     left = []
-    for y in range(len(chains) - LAG, len(chains)):
-        by, cby = chains[y]
-        left += max_block(by, cby, first=False)
+    if with_max:
+        for y in range(len(chains) - LAG, len(chains)):
+            by, cby = chains[y]
+            left += max_block(by, cby, first=False)
     return left
 
 
@@ -333,18 +393,19 @@ def shift_block(st, b, sh, first):
         st.emit(valu(f"v_xor_b32 {NEGM(b, i)}, 0x80000000, {MREF[b]}", r=[MREF[b]], w=[NEGM(b, i)]))
 
 
-def phase_b(st, p, nb, leftover, label_slow, label_end):
-    """PV(j) of nb blocks from vbuf[p]; the rescale decision at DEC_GAP; exp2
-    of S(j+1) after it"""
+def phase_b(st, p, pv, ex, leftover, dec_gap, label_slow, label_end):
+    """PV(j) of the blocks `pv` from vbuf[p]; the rescale decision over the
+    blocks `ex` (those with a QK(j+1)) at dec_gap, exp2 of their S(j+1)
+    after it.  No ex (the drain): the PV alone."""
     vb = VBUF[p]
-    mf, frag_first = pv_mfmas(nb)
+    mf, frag_first = pv_mfmas(pv)
     n = len(mf)
     gaps = {}
 
     def put(k, ins):
         gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
 
-    va = vahead(nb)
+    va = vahead(len(pv))
     for f in range(va, 2 * NE):
         k = frag_first[f - va]
         r = v_reads(f, vb)
@@ -352,27 +413,31 @@ def phase_b(st, p, nb, leftover, label_slow, label_end):
         put(k + 2, r[1])
     for i, ins in enumerate(leftover):
         put(LEFT_OFF + i, ins)
-    assert LEFT_OFF + len(leftover) - 1 <= DEC_GAP
-    if nb == 2:
+    assert not leftover or LEFT_OFF + len(leftover) - 1 <= dec_gap
+    if not ex:
+        st.interleave(mf, gaps)
+        st.branch("s_branch", label_end)
+        return
+    if len(ex) == 2:
         dec = [valu(f"v_max_f32 {T[0]}, {RMAX[0]}, {RMAX[1]}", r=RMAX, w=[T[0]]),
                valu(f"v_cmp_lt_f32 vcc, {RESCALE}, {T[0]}", r=[T[0]])]
     else:
-        dec = [valu(f"v_cmp_lt_f32 vcc, {RESCALE}, {RMAX[0]}", r=[RMAX[0]])]
-    ex = [e for b in range(nb) for e in exp_ops(b)]
-    n_g = n - DEC_GAP
-    for i, e in enumerate(ex):
-        put(DEC_GAP + 1 + (i * n_g) // len(ex), e)
-    for k in range(DEC_GAP):
+        dec = [valu(f"v_cmp_lt_f32 vcc, {RESCALE}, {RMAX[ex[0]]}", r=[RMAX[ex[0]]])]
+    exs = [e for b in ex for e in exp_ops(b)]
+    n_g = n - dec_gap
+    for i, e in enumerate(exs):
+        put(dec_gap + 1 + (i * n_g) // len(exs), e)
+    for k in range(dec_gap):
         for f in gaps.get(k, []):
             st.emit(f)
         st.emit(mf[k])
-    for f in gaps.get(DEC_GAP, []):
+    for f in gaps.get(dec_gap, []):
         st.emit(f)
     for d in dec:
         st.emit(d)
     st.branch("s_cbranch_vccnz", label_slow)
-    for k in range(DEC_GAP, n):
-        if k > DEC_GAP:
+    for k in range(dec_gap, n):
+        if k > dec_gap:
             for f in gaps.get(k, []):
                 st.emit(f)
         st.emit(mf[k])
@@ -381,8 +446,8 @@ def phase_b(st, p, nb, leftover, label_slow, label_end):
     st.branch("s_branch", label_end)
     # slow path: the remaining PV MFMAs (their V reads, no exps), then rescale
     st.label(label_slow)
-    for k in range(DEC_GAP, n):
-        if k > DEC_GAP:
+    for k in range(dec_gap, n):
+        if k > dec_gap:
             for f in gaps.get(k, []):
                 if isinstance(f, str) or f.kind != "trans":
                     st.emit(f)
@@ -390,14 +455,14 @@ def phase_b(st, p, nb, leftover, label_slow, label_end):
     for f in gaps.get(n, []):
         if isinstance(f, str) or f.kind != "trans":
             st.emit(f)
-    slow_softmax(st, range(nb), first=False)
-    for e in ex:
+    slow_softmax(st, ex, first=False)
+    for e in exs:
         st.emit(e)
     st.branch("s_branch", label_end)
 
 
 # ---------------------------------------------------------------------------
-# the generic iteration (a block's masked last QK^T, its PV drain)
+# iteration kinds
 # ---------------------------------------------------------------------------
 def mask_block(st, b, causal):
     """S(b) = -inf where key >= kv_hi_b or (causal) key > query row, for the
@@ -429,8 +494,8 @@ def full_max(st, b):
 
 
 def qk_plain(st, kb, blocks):
-    """QK^T of one tile for `blocks`, not interleaved: per 16-key block its
-    four K fragments, then the chains (the next block's reads ahead)"""
+    """QK^T of one tile for `blocks`, not interleaved (prologue): per 16-key
+    block its four K fragments were read one block ahead"""
     for t in range(NT):
         st.emit(k_read(t, 0, kb))
     for cb in range(4):
@@ -442,77 +507,39 @@ def qk_plain(st, kb, blocks):
                 st.emit(m)
 
 
-def pv_plain(st, vb, blocks):
-    mf, frag_first = pv_mfmas(len(blocks))
-    assert list(blocks) == list(range(len(blocks)))
-    gaps = {}
-    va = 6
-    for f in range(2 * NE):
-        k = 0 if f < va else frag_first[f - va] + 1
-        for i, r in enumerate(v_reads(f, vb)):
-            gaps.setdefault(k if f < va else k + i, []).append(r)
-    st.interleave(mf, gaps)
+# iteration kinds: (qk blocks, blocks with P(j) / PV(j), blocks whose QK(j+1)
+# tile is their last -- masked --); steady kinds have no mask
+KINDS = {
+    "s2": ((0, 1), (0, 1), ()),    # both blocks in their key range
+    "s1": ((0,), (0,), ()),        # block 0 alone (block 1 done / absent)
+    "A": ((0, 1), (0, 1), (1,)),   # block 1's last tile (causal diagonal)
+    "A2": ((0, 1), (0, 1), (0, 1)),  # both blocks' last tile (non-causal pair)
+    "B": ((0,), (0, 1), ()),       # block 1's PV drain beside block 0's QK
+    "B2": ((0,), (0, 1), (0,)),    # ... and block 0's last tile
+    "C": ((0,), (0,), (0,)),       # block 0's last tile
+    "D": ((), (0,), ()),           # block 0's PV drain
+    "D2": ((), (0, 1), ()),        # both blocks' PV drain
+}
 
 
-def dma_plain(st, p):
-    pairs, adv = dma_pieces(p)
-    for m0, ld in pairs:
-        st.emit(m0)
-        st.nop(1)
-        st.emit(ld)
-    for two in adv:
-        for ins in two:
-            st.emit(ins)
-
-
-def generic(st, p, causal):
-    """iteration j with a block boundary: P(j) of the blocks with a PV(j),
-    QK^T(j+1) of the blocks with a key tile j+1 (none: the drain), PV(j),
-    then the mask / maxima / rescale decision / exp2 of S(j+1) per block"""
-    kb, vb = KBUF[1 - p], VBUF[p]
-    nocvt1, noqk, qk1, qkdone = (w4.newlabel(x) for x in ("gnocvt1", "gnoqk", "gqk1", "gqkdone"))
-    pv1, pvdone, gend = (w4.newlabel(x) for x in ("gpv1", "gpvdone", "gend"))
-    for cb in range(4):
-        for c in cvt_block(0, cb):
-            st.emit(c)
-    st.raw(f"s_cmp_lt_u32 {SJ}, %[tl]")
-    st.branch("s_cbranch_scc0", nocvt1)
-    for cb in range(4):
-        for c in cvt_block(1, cb):
-            st.emit(c)
-    st.label(nocvt1)
-    st.raw(f"s_cmp_lt_u32 {SJ1}, %[th]")
-    st.branch("s_cbranch_scc0", noqk)
-    dma_plain(st, p)
-    st.raw(f"s_cmp_lt_u32 {SJ1}, %[tl]")
-    st.branch("s_cbranch_scc0", qk1)
-    qk_plain(st, kb, [0, 1])
-    st.branch("s_branch", qkdone)
-    st.label(qk1)
-    qk_plain(st, kb, [0])
-    st.label(qkdone)
-    st.label(noqk)
-    st.raw(f"s_cmp_lt_u32 {SJ}, %[tl]")
-    st.branch("s_cbranch_scc0", pv1)
-    pv_plain(st, vb, [0, 1])
-    st.branch("s_branch", pvdone)
-    st.label(pv1)
-    pv_plain(st, vb, [0])
-    st.label(pvdone)
-    # softmax of S(j+1), block 0 then (if it has the tile) block 1
-    st.raw(f"s_cmp_lt_u32 {SJ1}, %[th]")
-    st.branch("s_cbranch_scc0", gend)
+def iteration(st, p, kind, causal, Lb):
+    qk, pv, masked = KINDS[kind]
+    stamp_path(st, {"s2": 0, "s1": 1}.get(kind, 2))
+    slow = Lb["slow_" + kind][p]
+    if not masked:
+        left = phase_a(st, p, list(qk), list(pv), list(pv), with_max=True, dma=bool(qk))
+        phase_b(st, p, list(pv), list(qk), left, DEC_GAP if qk else 0, slow, Lb["end"][p])
+        return
+    # a block's last tile: QK^T without the running maxima, the limit mask on
+    # the blocks whose tile it is, the maxima of every QK block, then PV with
+    # the decision ahead of its first MFMA (gen_w4_item's general path)
+    phase_a(st, p, list(qk), list(pv), list(pv), with_max=False, dma=True)
     st.raw(f"s_lshl_b32 {KV0}, {SJ1}, 6")
-    for b in range(2):
-        if b == 1:
-            st.raw(f"s_cmp_lt_u32 {SJ1}, %[tl]")
-            st.branch("s_cbranch_scc0", gend)
+    for b in masked:
         mask_block(st, b, causal)
+    for b in qk:
         full_max(st, b)
-        slow_softmax(st, [b], first=False)
-        for e in exp_ops(b):
-            st.emit(e)
-    st.label(gend)
+    phase_b(st, p, list(pv), list(qk), [], 0, slow, Lb["end"][p])
 
 
 # ---------------------------------------------------------------------------
@@ -553,6 +580,10 @@ def q_scale(st):
 def prologue(st, causal):
     """descriptors, Q (both blocks) / K(0) / V(0) / K(1) loads, Q scaling,
     S(0) = K(0) Q^T with the tile-0 mask and the first-tile softmax"""
+    if STAMPS:
+        for r in range(72, NS_DIAG):
+            st.raw(f"s_mov_b32 s{r}, 0")
+        stamp_now(st, 76)
     st.raw(f"s_mov_b32 {SM0}, m0")
     st.raw(f"v_mov_b32 {KD(0)}, %[kdma]")
     st.raw(f"v_mov_b32 {VD(0)}, %[vdma]")
@@ -631,7 +662,12 @@ def prologue(st, causal):
         if b == 1:
             st.raw("s_cmp_eq_u32 %[tl], 0")
             st.branch("s_cbranch_scc1", blk1)
+        # tile 0 needs the limit mask only when it is the block's last tile
+        nomask = w4.newlabel(f"nomask{b}")
+        st.raw(f"s_cmp_eq_u32 {'%[th]' if b == 0 else '%[tl]'}, 1")
+        st.branch("s_cbranch_scc0", nomask)
         mask_block(st, b, causal)
+        st.label(nomask)
         slow_softmax(st, [b], first=True)
         for e in exp_ops(b):
             st.emit(e)
@@ -640,6 +676,9 @@ def prologue(st, causal):
     st.lgkm_all()
     st.raw("s_barrier")
     st.raw(f"s_mov_b32 {SJ}, 0")
+    if STAMPS:
+        stamp_now(st, 72)
+        st.raw("s_sub_u32 s85, s72, s76")
 
 
 def epilogue_block(st, b):
@@ -686,29 +725,45 @@ def epilogue_block(st, b):
 
 # ---------------------------------------------------------------------------
 def body(st, p, causal, Lb):
-    """iteration j (parity p = j & 1): steady with both blocks, steady with
-    block 0 alone, or generic; then the stage's DMA wait and the barrier"""
+    """iteration j (parity p = j & 1), one of KINDS by where j stands against
+    T0 = %[th] and T1 = %[tl] (T1 <= T0; T1 = 0: no block 1); then the
+    stage's DMA wait and the barrier"""
+    K = lambda k: Lb["k_" + k][p]  # noqa: E731
     st.label(Lb["loop"][p], drain_lgkm=True)
     st.raw(f"s_add_u32 {SJ1}, {SJ}, 1")
     st.raw(f"s_add_u32 {ST0}, {SJ}, 2")
-    st.raw(f"s_cmp_lt_u32 {ST0}, %[tl]")       # j+2 < T1: both blocks steady
-    st.branch("s_cbranch_scc1", Lb["s2"][p])
-    st.raw(f"s_cmp_lt_u32 {SJ}, %[tl]")         # block 1 still has PV(j)
-    st.branch("s_cbranch_scc1", Lb["gen"][p])
-    st.raw(f"s_cmp_lt_u32 {ST0}, %[th]")        # j+2 < T0: block 0 steady alone
-    st.branch("s_cbranch_scc1", Lb["s1"][p])
-    st.branch("s_branch", Lb["gen"][p])
-    st.label(Lb["s2"][p])
-    left = phase_a(st, p, 2)
-    phase_b(st, p, 2, left, Lb["slow2"][p], Lb["end"][p])
-    st.label(Lb["s1"][p])
-    left = phase_a(st, p, 1)
-    phase_b(st, p, 1, left, Lb["slow1"][p], Lb["end"][p])
-    st.label(Lb["gen"][p])
-    generic(st, p, causal)
+    st.raw(f"s_cmp_lt_u32 {ST0}, %[tl]")       # j+2 < T1: both steady
+    st.branch("s_cbranch_scc1", K("s2"))
+    st.raw(f"s_cmp_eq_u32 {ST0}, %[tl]")       # j+2 == T1: block 1's last tile
+    st.branch("s_cbranch_scc0", Lb["d1"][p])
+    st.raw("s_cmp_eq_u32 %[tl], %[th]")
+    st.branch("s_cbranch_scc1", K("A2"))
+    st.branch("s_branch", K("A"))
+    st.label(Lb["d1"][p])
+    st.raw(f"s_cmp_eq_u32 {SJ1}, %[tl]")       # j+1 == T1: block 1's drain
+    st.branch("s_cbranch_scc0", Lb["d2"][p])
+    st.raw(f"s_cmp_lt_u32 {ST0}, %[th]")
+    st.branch("s_cbranch_scc1", K("B"))
+    st.raw(f"s_cmp_eq_u32 {ST0}, %[th]")
+    st.branch("s_cbranch_scc1", K("B2"))
+    st.branch("s_branch", K("D2"))
+    st.label(Lb["d2"][p])
+    st.raw(f"s_cmp_lt_u32 {ST0}, %[th]")       # j+2 < T0: block 0 steady alone
+    st.branch("s_cbranch_scc1", K("s1"))
+    st.raw(f"s_cmp_eq_u32 {ST0}, %[th]")
+    st.branch("s_cbranch_scc1", K("C"))
+    st.branch("s_branch", K("D"))
+    for kind in KINDS:
+        st.label(K(kind))
+        iteration(st, p, kind, causal, Lb)
     st.label(Lb["end"][p], drain_lgkm=True)
+    stamp_path_end(st)
     st.raw("s_waitcnt vmcnt(0)")   # this iteration's LDS-DMA landed before the barrier publishes it
     st.raw("s_barrier")
+    if STAMPS:
+        stamp_now(st, 72)
+        st.raw("s_sub_u32 s75, s72, s76")
+        st.raw("s_add_u32 s84, s84, s75")
     st.raw(f"s_add_u32 {SJ}, {SJ}, 1")
     st.raw(f"s_cmp_lt_u32 {SJ}, %[th]")
     if p == 0:
@@ -720,18 +775,31 @@ def body(st, p, causal, Lb):
 def generate(causal):
     st = Stream()
     Lb = {k: [w4.newlabel(f"{k}{p}") for p in range(2)]
-          for k in ("loop", "s2", "s1", "gen", "slow2", "slow1", "end")}
+          for k in ["loop", "end", "d1", "d2"] + [f"k_{x}" for x in KINDS] + [f"slow_{x}" for x in KINDS]}
     Lb["done"] = w4.newlabel("done")
     prologue(st, causal)
     body(st, 0, causal, Lb)
     body(st, 1, causal, Lb)
     st.label(Lb["done"], drain_lgkm=True)
+    stamp_now(st, 76)
     epilogue_block(st, 0)
     nob1 = w4.newlabel("nob1")
     st.raw("s_cmp_eq_u32 %[tl], 0")
     st.branch("s_cbranch_scc1", nob1)
     epilogue_block(st, 1)
     st.label(nob1)
+    if STAMPS:
+        st.raw("s_waitcnt vmcnt(0)")
+        stamp_now(st, 72)
+        st.raw("s_sub_u32 s86, s72, s76")
+        st.raw(f"s_lshl_b32 {ST1}, {QR[0]}, 8")
+        for i in range(16):
+            st.raw(f"v_mov_b32 v{i}, s{78 + i}")
+        st.raw(f"v_mov_b32 v16, {ST1}")
+        st.nop(2)
+        for i in range(4):
+            st.raw(f"buffer_store_dwordx4 v[{4 * i}:{4 * i + 3}], v16, {RO}, 0 offen offset:{16 * i}")
+        st.raw("s_waitcnt vmcnt(0)")
     st.raw(f"s_mov_b32 m0, {SM0}")
     return st.out
 
@@ -747,7 +815,7 @@ def cxx(causal, bf16, lines):
     body_ = "\n".join(f'      "{ln}\\n"' for ln in lines)
     vclob = ", ".join(f'"v{i}"' for i in range(NV))
     aclob = ", ".join(f'"a{i}"' for i in range(NA))
-    sclob = ", ".join(f'"s{i}"' for i in range(NS_LO, NS_HI))
+    sclob = ", ".join(f'"s{i}"' for i in range(NS_LO, NS_DIAG if STAMPS else NS_HI))
     name = ("w4p_item_causal" if causal else "w4p_item_noncausal") + ("_bf16" if bf16 else "_f16")
     return f"""
 __device__ __forceinline__ void {name}(const W4PRun& rn, const W4Lane& ln) {{

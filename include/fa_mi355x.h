@@ -150,11 +150,19 @@ int fa_fwd_bf16_ws(const void* q, const void* k, const void* v, void* o,
  * instead: check fa_fwd_split_pieces() first (> 0: the split tier runs with
  * that many 64-key tiles per piece, and this config is not used).
  *
+ * The answer depends on the shape and on the CU count of the calling
+ * thread's current HIP device (the W4 tier's tail and the paired tier's
+ * one-round test size the grid from it, as the launch does; 256 if the
+ * query fails).  The tier is the same for fp16 and bf16; fa_fwd_f16 /
+ * fa_fwd_bf16 at head_dim 64 run the head_dim-64 twin of this tier, or of
+ * the tier below it when this one has none (the paired tier: head_dim 128).
+ *
  * Config ids are positions in this build's table (fa_num_configs /
  * fa_config_info): they are not stable across releases (round 3 renumbered
  * 0-49 to 0-43 when the table was trimmed to the dispatched tiers; round 4
- * appended the head_dim-64 W4 configs 44-47).  Select a
- * tier by its fa_config_info().name, not by a remembered id. */
+ * appended the head_dim-64 W4 configs 44-47; round 5 the paired
+ * short-sequence configs 48-51).  Select a tier by its
+ * fa_config_info().name, not by a remembered id. */
 int fa_select_config(int batch, int heads, int seq_len, int causal);
 
 int fa_num_configs(void);

@@ -107,19 +107,24 @@ def test_select_config(causal):
             cid = fa.select_config(b, h, s, causal)
             c = cfgs[cid]
             assert c.causal == causal and not c.split_kv
-    # B=1 H=32: the short, under-filled launches go to the KV-pair kernel,
-    # the long ones to the 256-row persistent ping-pong
-    assert "_kvpair_" in cfgs[fa.select_config(1, 32, 1024, causal)].name
+    # B=1 H=32 S=1024 (BASELINE config 1): the paired tier (one round of
+    # pairs); the long launches: the persistent tier
+    assert "_asm_pair_" in cfgs[fa.select_config(1, 32, 1024, causal)].name
     assert "_persistent_" in cfgs[fa.select_config(1, 32, 8192, causal)].name
-    # launches of <= 256 64-row blocks: the KV-quad; S=256: the 4-wave loop
-    assert "_kvquad_" in cfgs[fa.select_config(1, 8, 2048, causal)].name
-    assert "_kvquad_" in cfgs[fa.select_config(1, 32, 512, causal)].name
+    # causal launches of <= 2 rounds of pairs up to S=2048: the paired tier;
+    # non-causal ones of <= 256 64-row blocks under 3/4 of a round: the KV-quad
+    short = "_asm_pair_" if causal else "_kvquad_"
+    assert short in cfgs[fa.select_config(1, 8, 2048, causal)].name
+    assert short in cfgs[fa.select_config(1, 32, 512, causal)].name
     assert "_w4_" in cfgs[fa.select_config(1, 32, 256, causal)].name
+    # more than a round of pairs: the KV-pair (non-causal) / 4-wave loop
+    assert "_kvpair_" in cfgs[fa.select_config(1, 36, 1024, False)].name
     # causal, two rounds of 64-row blocks over long heads: the KV-quad's
-    # four-way key split; non-causal (and S=1024) stay on the KV-pair
+    # four-way key split; non-causal stays on the KV-pair
     want = "_kvquad_" if causal else "_kvpair_"
-    for b, h, s in ((1, 4, 8192), (1, 2, 16384), (1, 8, 4096), (1, 16, 2048)):
+    for b, h, s in ((1, 4, 8192), (1, 2, 16384), (1, 8, 4096)):
         assert want in cfgs[fa.select_config(b, h, s, causal)].name, (b, h, s, causal)
+    assert "_asm_pair_" in cfgs[fa.select_config(1, 16, 2048, causal)].name  # 256 pairs
 
 
 def _null_call(lib, head_dim=128, b=1, h=1, s=64, causal=0, ptr=None):
@@ -260,7 +265,7 @@ def test_config_table_ships_only_used_tiers():
     # every dispatched fp16 d128 tier has all three twins (W4: the bf16 one)
     for name in used:
         if not name.startswith(("bf16_", "d64_")):
-            pres = ("bf16_",) if name in w4 else TWIN_PREFIXES
+            pres = ("bf16_",) if "_asm_" in name else TWIN_PREFIXES  # W4 / W4P: bf16 only
             assert all(pre + name in by_name for pre in pres), name
 
 
@@ -359,6 +364,27 @@ def test_generated_item_program_is_current(tmp_path):
     with open(os.path.join(csrc, "fa_w4_item.inc")) as f:
         committed = f.read()
     assert out.read_text() == committed, "fa_w4_item.inc is stale: run `make -C flash-attention-cuda_amd`"
+
+
+def test_generated_pair_program_is_current(tmp_path):
+    """The committed paired-tier program (csrc/fa_w4p_item.inc) is exactly what
+    csrc/gen_w4p_item.py generates, and its stamps variant generates."""
+    import sys
+
+    csrc = os.path.join(ROOT, "flash-attention-cuda_amd", "csrc")
+    env = {k: v for k, v in os.environ.items() if not k.startswith("W4")}
+    out = tmp_path / "fa_w4p_item.inc"
+    subprocess.run([sys.executable, os.path.join(csrc, "gen_w4p_item.py"), str(out)], check=True,
+                   env=env, timeout=300)
+    with open(os.path.join(csrc, "fa_w4p_item.inc")) as f:
+        assert out.read_text() == f.read(), "fa_w4p_item.inc is stale: run `make -C flash-attention-cuda_amd`"
+    env["W4P_DIAG"] = "stamps"
+    subprocess.run([sys.executable, os.path.join(csrc, "gen_w4p_item.py"), str(out)], check=True,
+                   env=env, timeout=300)
+    text = out.read_text()
+    for fn in ("w4p_item_causal_f16", "w4p_item_noncausal_bf16"):
+        assert f"void {fn}(" in text, fn
+    assert "s_memtime" in text
 
 
 @pytest.mark.parametrize("env", [
