@@ -656,16 +656,22 @@ static int select_tier(int batch, int heads, int seq_len, int causal, bool pair)
     return cfg_for(256, 4, 64, c, 0, 5);
   }
   if (seq_len <= 256) return cfg_for(128, 4, 64, c, 0, 0);
-  // paired 64-row query blocks (W4P, fa_w4p_kernel.hpp): causal launches of
-  // at most two rounds of pairs on the device's CUs (every pair
-  // costs nqb64+1 key tiles; past two rounds the KV-pair's 8 waves win: B=4
-  // H=32 S=1024 709 vs 522), non-causal ones of one nearly full round (B=1
-  // H=32 S=1024 792 vs 670; at half a round the KV-quad/pair win: H=16 474
-  // vs 514); S <= 2048 (longer heads: measured against the KV-quad first)
-  // (profiles/r05_w4p_*ab*.jsonl)
+  // paired 64-row query blocks (W4P, fa_w4p_kernel.hpp), same-process A/Bs
+  // against the KV-pair / KV-quad / split tiers (profiles/r05_w4p_*ab*.jsonl):
+  //  * causal, S <= 2048, at most two rounds of pairs on the CUs (every pair
+  //    costs nqb64+1 key tiles): B=1 H=32 S=1024 530 vs 388, B=2 H=8 S=2048
+  //    673 vs 507, H=24 S=1024 429 vs 315; past two rounds the KV-pair /
+  //    persistent tiers win (B=4 H=32 S=1024 522 vs 709);
+  //  * causal, S <= 4096 in one round: B=1 H=8 S=4096 755 vs KV-quad 667 and
+  //    split 714; longer heads stay on the split tier / KV-quad (H=4 S=8192
+  //    742 vs 884 / 785, H=12 S=4096 717 vs 779);
+  //  * non-causal from 3/4 of a round of pairs (below, the KV-quad: H=16
+  //    S=1024 470 vs 514) up to the persistent tier: H=4 S=8192 1182 vs 1090,
+  //    H=16 S=2048 1004 vs 899, H=48 S=512 557 vs 468
   if (pair) {
     const long long nq64 = (seq_len + 63) / 64, pairs = bh * ((nq64 + 1) / 2), cus = num_cus();
-    if (nq64 <= 32 && (causal ? pairs <= 2 * cus : (4 * pairs >= 3 * cus && pairs <= cus)))
+    if (causal ? ((nq64 <= 32 && pairs <= 2 * cus) || (nq64 <= 64 && pairs <= cus))
+               : 4 * pairs >= 3 * cus)
       return cfg_for(128, 4, 64, c, 0, 6);
   }
   // causal, two rounds of 64-row blocks over long heads (>= 32 blocks per
@@ -791,6 +797,8 @@ static SplitPlan split_plan(int batch, int heads, int seq_len, int head_dim, int
   const int nqb = (seq_len + 255) / 256;
   const long long wg256 = bh * nqb;
   if (seq_len < 4096 || wg256 >= 384) return none;  // short, or the persistent tier's shapes
+  // the paired tier's shapes (B=1 H=8 S=4096: 755 vs the split's 714)
+  if (kConfigs[select_tier(batch, heads, seq_len, causal, true)].kind == 6) return none;
   const long long cus = num_cus();
   // the shortest piece (>= 4 tiles: the diagonal piece keeps every wave
   // busy) whose pieces all fit one round on the device's CUs

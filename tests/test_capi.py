@@ -117,14 +117,17 @@ def test_select_config(causal):
     assert short in cfgs[fa.select_config(1, 8, 2048, causal)].name
     assert short in cfgs[fa.select_config(1, 32, 512, causal)].name
     assert "_w4_" in cfgs[fa.select_config(1, 32, 256, causal)].name
-    # more than a round of pairs: the KV-pair (non-causal) / 4-wave loop
-    assert "_kvpair_" in cfgs[fa.select_config(1, 36, 1024, False)].name
-    # causal, two rounds of 64-row blocks over long heads: the KV-quad's
-    # four-way key split; non-causal stays on the KV-pair
-    want = "_kvquad_" if causal else "_kvpair_"
-    for b, h, s in ((1, 4, 8192), (1, 2, 16384), (1, 8, 4096)):
+    # between the KV-quad's and the paired tier's non-causal shapes: the KV-pair
+    assert "_kvpair_" in cfgs[fa.select_config(1, 20, 1024, False)].name
+    # long heads, few of them: causal -> the KV-quad's four-way key split
+    # (the _ws entries run the split tier there), non-causal -> the paired tier
+    want = "_kvquad_" if causal else "_asm_pair_"
+    for b, h, s in ((1, 4, 8192), (1, 2, 16384)):
         assert want in cfgs[fa.select_config(b, h, s, causal)].name, (b, h, s, causal)
-    assert "_asm_pair_" in cfgs[fa.select_config(1, 16, 2048, causal)].name  # 256 pairs
+    for b, h, s in ((1, 16, 2048), (1, 8, 4096), (2, 8, 2048)):  # <= 1 round of pairs
+        assert "_asm_pair_" in cfgs[fa.select_config(b, h, s, causal)].name, (b, h, s, causal)
+    if causal:  # more than a round at S=4096: the KV-pair
+        assert "_kvpair_" in cfgs[fa.select_config(1, 12, 4096, True)].name
 
 
 def _null_call(lib, head_dim=128, b=1, h=1, s=64, causal=0, ptr=None):
@@ -238,7 +241,7 @@ def test_config_table_ships_only_used_tiers():
     for causal in (False, True):
         for s in (1, 64, 128, 200, 256, 300, 512, 768, 1024, 2048, 4096, 8192, 16384, 32768):
             for b, h in ((1, 1), (1, 2), (1, 4), (1, 8), (1, 16), (1, 32), (1, 64), (2, 32),
-                         (4, 32), (8, 32), (16, 32), (64, 32), (3, 40), (1, 203)):
+                         (4, 32), (8, 32), (16, 32), (64, 32), (3, 40), (1, 203), (1, 20)):
                 base = cfgs[fa.select_config(b, h, s, causal)].name
                 used |= {pre + base for pre in TWIN_PREFIXES if pre + base in by_name}
     baselines = {"bm256_bn64_w8_m16_pingpong_noncausal", "bm256_bn64_w8_m16_pingpong_causal",
@@ -303,14 +306,16 @@ def test_split_plan_and_workspace_entry():
     fa = _fa()
     lib = fa.load_library()
     # the dispatcher splits long causal launches short of the persistent tier
-    for b, h, s in ((1, 4, 4096), (1, 8, 4096), (1, 4, 8192), (1, 2, 16384), (1, 1, 32768)):
+    for b, h, s in ((1, 12, 4096), (1, 4, 8192), (1, 2, 16384), (1, 1, 32768)):
         t = lib.fa_fwd_split_pieces(b, h, s, 128, 1)
         assert t >= 4, (b, h, s)
         need = lib.fa_fwd_ws_bytes(b, h, s, 128, 1, 0)
         assert need > 0 and need % 256 == 0
     # no split: non-causal, head_dim 64, the persistent tier's shapes, S < 4096
+    # and the paired tier's shapes (B=1 H<=8 S=4096)
     for args in ((1, 4, 4096, 128, 0), (1, 4, 4096, 64, 1), (64, 32, 4096, 128, 1),
-                 (1, 32, 8192, 128, 1), (1, 32, 1024, 128, 1), (1, 8, 2048, 128, 1)):
+                 (1, 32, 8192, 128, 1), (1, 32, 1024, 128, 1), (1, 8, 2048, 128, 1),
+                 (1, 8, 4096, 128, 1), (1, 4, 4096, 128, 1)):
         assert lib.fa_fwd_split_pieces(*args) == 0, args
         assert lib.fa_fwd_ws_bytes(*args, 0) == 0, args
     # a forced piece length: sizes grow with the pieces per block; > 8 pieces,
@@ -319,14 +324,14 @@ def test_split_plan_and_workspace_entry():
     assert lib.fa_fwd_ws_bytes(1, 32, 1024, 128, 1, 1) == 0   # 16 pieces
     assert lib.fa_fwd_ws_bytes(1, 32, 1024, 128, 0, 6) == 0
     assert lib.fa_fwd_ws_bytes(1, 32, 1024, 128, 1, 16) == 0  # one piece
-    need = lib.fa_fwd_ws_bytes(1, 4, 4096, 128, 1, 0)
+    need = lib.fa_fwd_ws_bytes(1, 4, 8192, 128, 1, 0)
     p = ctypes.c_void_p(0x1000)
-    assert lib.fa_fwd_f16_ws(p, p, p, p, 1, 4, 4096, 128, 1, 0, None, need, None) == fa.FA_ERR_WORKSPACE
-    assert lib.fa_fwd_f16_ws(p, p, p, p, 1, 4, 4096, 128, 1, 0, p, need - 1, None) == fa.FA_ERR_WORKSPACE
+    assert lib.fa_fwd_f16_ws(p, p, p, p, 1, 4, 8192, 128, 1, 0, None, need, None) == fa.FA_ERR_WORKSPACE
+    assert lib.fa_fwd_f16_ws(p, p, p, p, 1, 4, 8192, 128, 1, 0, p, need - 1, None) == fa.FA_ERR_WORKSPACE
     assert lib.fa_fwd_f16_ws(p, p, p, p, 1, 32, 1024, 128, 1, 1, p, 1 << 30, None) == fa.FA_ERR_BAD_CONFIG
-    assert lib.fa_fwd_bf16_ws(p, p, p, p, 1, 4, 4096, 96, 1, 0, p, need, None) == \
+    assert lib.fa_fwd_bf16_ws(p, p, p, p, 1, 4, 8192, 96, 1, 0, p, need, None) == \
         fa.FA_ERR_UNSUPPORTED_HEAD_DIM
-    assert lib.fa_fwd_f16_ws(None, p, p, p, 1, 4, 4096, 128, 1, 0, p, need, None) == fa.FA_ERR_NULL_POINTER
+    assert lib.fa_fwd_f16_ws(None, p, p, p, 1, 4, 8192, 128, 1, 0, p, need, None) == fa.FA_ERR_NULL_POINTER
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")

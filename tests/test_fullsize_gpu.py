@@ -86,10 +86,11 @@ def test_max_sequence_sampled_rows(s, h, causal, head_dim):
 @pytest.mark.parametrize("b,h,s", [(1, 4, 8192), (1, 2, 16384), (1, 8, 4096), (2, 8, 2048)])
 def test_long_causal_few_heads_kvquad(b, h, s):
     # the selector sends these causal launches to the KV-quad (four-way key
-    # split over long heads): sampled rows of every head against the oracle
+    # split over long heads) or, at up to one round of 64-row pairs, to the
+    # paired tier: sampled rows of every head against the oracle
     fa = _fa()
     cfg = fa.configs()[fa.select_config(b, h, s, True)].name
-    assert "_kvquad_" in cfg, cfg
+    assert ("_asm_pair_" if s <= 4096 else "_kvquad_") in cfg, cfg
     shape = (b, h, s, 128)
     q, k, v = _rand(shape, 31), _rand(shape, 32), _rand(shape, 33)
     o = fa.flash_attention_fwd(q, k, v, causal=True)

@@ -55,7 +55,7 @@ def _torch_ref(q, k, v):
 # launches short of the persistent tier); > 0 forces that piece length, so
 # short and ragged shapes, 2..8 pieces per block and pieces shorter than the
 # diagonal's 4 tiles are covered too
-SHAPES = [(1, 4, 4096, 0), (1, 8, 4096, 0), (2, 3, 5000, 0), (1, 32, 512, 4), (1, 32, 768, 4),
+SHAPES = [(1, 12, 4096, 0), (1, 8, 4096, 22), (2, 3, 5000, 0), (1, 4, 8192, 0), (1, 32, 512, 4), (1, 32, 768, 4),
           (1, 32, 1024, 6), (2, 8, 1000, 5), (1, 16, 2048, 12), (3, 5, 1500, 4), (1, 1, 512, 4),
           (1, 2, 2048, 4), (2, 2, 700, 2), (1, 3, 512, 1)]
 
@@ -81,7 +81,7 @@ def test_split_matches_oracle(shape):
     assert err <= TOL, err
 
 
-@pytest.mark.parametrize("shape", [(1, 32, 1024, 6), (2, 8, 1000, 4), (1, 4, 4096, 0)],
+@pytest.mark.parametrize("shape", [(1, 32, 1024, 6), (2, 8, 1000, 4), (1, 4, 4096, 22)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_split_peaked(shape):
     # Q, K x4: row maxima grow past the lazy-rescale threshold inside pieces
@@ -95,7 +95,7 @@ def test_split_peaked(shape):
     assert err <= TOL, err
 
 
-@pytest.mark.parametrize("shape", [(1, 32, 1024, 6), (2, 8, 1000, 4), (1, 8, 4096, 0)],
+@pytest.mark.parametrize("shape", [(1, 32, 1024, 6), (2, 8, 1000, 4), (1, 12, 4096, 0)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_split_bf16(shape):
     fa = _fa()
@@ -113,7 +113,7 @@ def test_split_workspace_reuse_and_streams():
     streams with their own workspaces: every result equals the first launch's
     (the arrival counters are back at zero after each launch)."""
     fa = _fa()
-    shapes = [(1, 4, 4096, 0), (1, 32, 1024, 6), (1, 32, 512, 4), (2, 8, 1000, 5)]
+    shapes = [(1, 4, 4096, 22), (1, 32, 1024, 6), (1, 32, 512, 4), (2, 8, 1000, 5)]
     data = {sh: [_rand(sh[:3] + (128,), 1300 + 3 * n + i) for i in range(3)] for n, sh in enumerate(shapes)}
     run = lambda sh: fa.flash_attention_fwd(*data[sh], causal=True, piece_tiles=sh[3])
     first = {sh: run(sh) for sh in shapes}
@@ -137,7 +137,7 @@ def test_split_workspace_reuse_and_streams():
 def test_split_c_entry_workspace_checks():
     fa = _fa()
     lib = fa.load_library()
-    b, h, s = 1, 4, 4096
+    b, h, s = 1, 4, 8192  # a shape the dispatcher splits (S=4096 at H<=8: the paired tier)
     need = lib.fa_fwd_ws_bytes(b, h, s, 128, 1, 0)
     assert need > 0
     q, k, v = (_rand((b, h, s, 128), 1400 + i) for i in range(3))

@@ -127,6 +127,36 @@ def test_pair_bf16(shape, causal):
     _check(*shape, causal, seed=730, dtype=torch.bfloat16)
 
 
+def _sample_rows(s, n=12):
+    rng = np.random.default_rng(s)
+    return sorted({0, 63, 64, s // 2, s - 64, s - 1} | set(int(x) for x in rng.integers(0, s, n)))
+
+
+@pytest.mark.parametrize("b,h,s,causal", [(1, 8, 4096, True), (1, 8, 4096, False), (2, 8, 2048, True),
+                                           (1, 4, 8192, False), (1, 1, 32768, False)])
+def test_pair_long_heads(b, h, s, causal):
+    """the dispatcher's long few-head shapes (one round of pairs): sampled rows
+    of every head against an fp32 torch reference of those rows, head 0's
+    against the oracle's row-sampled entry"""
+    fa = _fa()
+    assert "_asm_pair_" in fa.configs()[fa.select_config(b, h, s, causal)].name
+    q, k, v = (_rand((b, h, s, 128), 760 + i) for i in range(3))
+    out = fa.flash_attention_fwd(q, k, v, causal=causal)
+    torch.cuda.synchronize()
+    rows = _sample_rows(s)
+    r = torch.tensor(rows, device=q.device)
+    for bi in range(b):
+        sc = q[bi][:, r].float() @ k[bi].float().transpose(-1, -2) / math.sqrt(128)
+        if causal:
+            keep = torch.arange(s, device=q.device)[None, :] <= r[:, None]
+            sc = sc.masked_fill(~keep, float("-inf"))
+        ref = torch.softmax(sc, dim=-1) @ v[bi].float()
+        err = (out[bi][:, r].float() - ref).abs().max().item()
+        assert err <= TOL, f"batch {bi}: max err {err}"
+    ro = oracle.attention_rows(_bits(q[0, 0]), _bits(k[0, 0]), _bits(v[0, 0]), rows, causal)
+    assert oracle.max_abs_diff(_bits(out[0, 0])[rows], ro) <= TOL
+
+
 def test_pair_causal_row0_and_ones():
     """causal row 0 sees key 0 only: O[0] = V[0] exactly; V = 1 -> O = 1"""
     fa = _fa()
