@@ -343,7 +343,8 @@ struct Config {
   int sched;  // 0 = one barrier per tile, 1 = 8-wave ping-pong, 3 = ping-pong + LDS-DMA tiles
   int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent, 3 = KV-pair,
               // 4 = KV-quad, 5 = persistent, one wave per SIMD (W4, asm item program),
-              // 6 = paired 64-row query blocks, one wave per SIMD (W4P, asm item program)
+              // 6 = paired 64-row query blocks, one wave per SIMD (W4P, asm item program),
+              // 7 = two pairs per workgroup (the same program)
   kernel_fn fn;
 };
 
@@ -352,7 +353,9 @@ constexpr kernel_fn pick_kernel() {
   if constexpr (KIND == 5)
     return fa_fwd_f16_w4_kernel<(C != 0), DT == 1, HDIM>;
   else if constexpr (KIND == 6)
-    return fa_fwd_w4p_kernel<(C != 0), DT == 1>;
+    return fa_fwd_w4p_kernel<(C != 0), DT == 1, 1>;
+  else if constexpr (KIND == 7)
+    return fa_fwd_w4p_kernel<(C != 0), DT == 1, 2>;
 
   else if constexpr (KIND == 3)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
@@ -393,10 +396,11 @@ constexpr kernel_fn pick_kernel() {
   {{ID, 256, 64, 4, C, 0, kW4LdsBytes, NAME, DT, HDIM}, 0, 5,                            \
    pick_kernel<4, 64, C, 5, 0, DT, HDIM>()}
 #define FA_CFG_W4(ID, C, DT, NAME) FA_CFG_W4D(ID, C, DT, 128, NAME)
-// W4P: 4 waves x (16 + 16) query rows of two 64-row blocks, K/V double-buffered (64 KB)
-#define FA_CFG_W4P(ID, C, DT, NAME)                                                    \
-  {{ID, 128, 64, 4, C, 0, kW4PLdsBytes, NAME, DT, 128}, 0, 6,                            \
-   pick_kernel<4, 64, C, 6, 0, DT, 128>()}
+// W4P: 4 waves x 16 query rows of each of two (G = 1) or four (G = 2) 64-row
+// blocks, K/V double-buffered (64 KB)
+#define FA_CFG_W4P(ID, G, C, DT, NAME)                                                 \
+  {{ID, 128 * (G), 64, 4, C, 0, kW4PLdsBytes, NAME, DT, 128}, 0, 5 + (G),                \
+   pick_kernel<4, 64, C, 5 + (G), 0, DT, 128>()}
 
 // Only tiers the dispatcher picks, explicit entry points (split-KV) and the
 // baselines a test compares against (the per-item ping-pong 2/3: the
@@ -458,10 +462,15 @@ static const Config kConfigs[] = {
     FA_CFG_W4D(46, 0, 1, 64, "bf16_d64_bm256_bn64_w4x64_m16_asm_persistent_noncausal"),
     FA_CFG_W4D(47, 1, 1, 64, "bf16_d64_bm256_bn64_w4x64_m16_asm_persistent_causal"),
     // paired 64-row query blocks, one wave per SIMD, asm item program (fa_w4p_kernel.hpp)
-    FA_CFG_W4P(48, 0, 0, "bm128_bn64_w4x32_m16_asm_pair_noncausal"),
-    FA_CFG_W4P(49, 1, 0, "bm128_bn64_w4x32_m16_asm_pair_causal"),
-    FA_CFG_W4P(50, 0, 1, "bf16_bm128_bn64_w4x32_m16_asm_pair_noncausal"),
-    FA_CFG_W4P(51, 1, 1, "bf16_bm128_bn64_w4x32_m16_asm_pair_causal"),
+    FA_CFG_W4P(48, 1, 0, 0, "bm128_bn64_w4x32_m16_asm_pair_noncausal"),
+    FA_CFG_W4P(49, 1, 1, 0, "bm128_bn64_w4x32_m16_asm_pair_causal"),
+    FA_CFG_W4P(50, 1, 0, 1, "bf16_bm128_bn64_w4x32_m16_asm_pair_noncausal"),
+    FA_CFG_W4P(51, 1, 1, 1, "bf16_bm128_bn64_w4x32_m16_asm_pair_causal"),
+    // two pairs per workgroup: four 64-row blocks, 16 rows of each per wave
+    FA_CFG_W4P(52, 2, 0, 0, "bm256_bn64_w4x64_m16_asm_quad_noncausal"),
+    FA_CFG_W4P(53, 2, 1, 0, "bm256_bn64_w4x64_m16_asm_quad_causal"),
+    FA_CFG_W4P(54, 2, 0, 1, "bf16_bm256_bn64_w4x64_m16_asm_quad_noncausal"),
+    FA_CFG_W4P(55, 2, 1, 1, "bf16_bm256_bn64_w4x64_m16_asm_quad_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -658,21 +667,24 @@ static int select_tier(int batch, int heads, int seq_len, int causal, bool pair)
   if (seq_len <= 256) return cfg_for(128, 4, 64, c, 0, 0);
   // paired 64-row query blocks (W4P, fa_w4p_kernel.hpp), same-process A/Bs
   // against the KV-pair / KV-quad / split tiers (profiles/r05_w4p_*ab*.jsonl):
-  //  * causal, S <= 2048, at most two rounds of pairs on the CUs (every pair
-  //    costs nqb64+1 key tiles): B=1 H=32 S=1024 530 vs 388, B=2 H=8 S=2048
-  //    673 vs 507, H=24 S=1024 429 vs 315; past two rounds the KV-pair /
-  //    persistent tiers win (B=4 H=32 S=1024 522 vs 709);
-  //  * causal, S <= 4096 in one round: B=1 H=8 S=4096 755 vs KV-quad 667 and
-  //    split 714; longer heads stay on the split tier / KV-quad (H=4 S=8192
-  //    742 vs 884 / 785, H=12 S=4096 717 vs 779);
+  //  * causal, S <= 4096, one round of pairs on the CUs (every pair costs
+  //    nqb64+1 key tiles): B=1 H=32 S=1024 530 vs 388, B=2 H=8 S=2048 673 vs
+  //    507, H=24 S=1024 429 vs 315, H=8 S=4096 755 vs KV-quad 667 and split
+  //    714; longer heads stay on the split tier / KV-quad (H=4 S=8192 742 vs
+  //    884 / 785);
   //  * non-causal from 3/4 of a round of pairs (below, the KV-quad: H=16
   //    S=1024 470 vs 514) up to the persistent tier: H=4 S=8192 1182 vs 1090,
   //    H=16 S=2048 1004 vs 899, H=48 S=512 557 vs 468
+  //  * causal launches of one to two rounds of pairs run them two per
+  //    workgroup (quads: four blocks per wave while the light blocks last,
+  //    two after): B=1 H=32 S=2048 816 vs pairs 663, B=2 H=32 S=1024 662 vs
+  //    532, H=16 S=4096 942 vs KV-pair 862; past that the persistent tier
+  //    (B=4 H=32 S=1024 802 vs 701)
   if (pair) {
     const long long nq64 = (seq_len + 63) / 64, pairs = bh * ((nq64 + 1) / 2), cus = num_cus();
-    if (causal ? ((nq64 <= 32 && pairs <= 2 * cus) || (nq64 <= 64 && pairs <= cus))
-               : 4 * pairs >= 3 * cus)
-      return cfg_for(128, 4, 64, c, 0, 6);
+    if (causal && nq64 <= 64 && pairs <= cus) return cfg_for(128, 4, 64, c, 0, 6);
+    if (causal && nq64 <= 64 && pairs <= 2 * cus) return cfg_for(256, 4, 64, c, 0, 7);
+    if (!causal && 4 * pairs >= 3 * cus) return cfg_for(128, 4, 64, c, 0, 6);
   }
   // causal, two rounds of 64-row blocks over long heads (>= 32 blocks per
   // head): the KV-quad's four-way key split halves the heaviest block's key
@@ -798,7 +810,7 @@ static SplitPlan split_plan(int batch, int heads, int seq_len, int head_dim, int
   const long long wg256 = bh * nqb;
   if (seq_len < 4096 || wg256 >= 384) return none;  // short, or the persistent tier's shapes
   // the paired tier's shapes (B=1 H=8 S=4096: 755 vs the split's 714)
-  if (kConfigs[select_tier(batch, heads, seq_len, causal, true)].kind == 6) return none;
+  if (kConfigs[select_tier(batch, heads, seq_len, causal, true)].kind >= 6) return none;
   const long long cus = num_cus();
   // the shortest piece (>= 4 tiles: the diagonal piece keeps every wave
   // busy) whose pieces all fit one round on the device's CUs

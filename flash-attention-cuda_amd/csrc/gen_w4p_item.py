@@ -1,30 +1,33 @@
 #!/usr/bin/env python3
-"""Generator of the paired one-wave-per-SIMD item program (fa_w4p_item.inc).
+"""Generator of the multi-block one-wave-per-SIMD item program (fa_w4p_item.inc).
 
 The short-sequence tier W4P (fa_w4p_kernel.hpp): one workgroup = 4 waves, one
-per SIMD, on TWO 64-row query blocks of one head, X0 and X1.  Wave w holds 16
-rows of each -- row block 0 = rows 64 X0 + 16 w + r16, row block 1 = rows
-64 X1 + 16 w + r16 -- and the four waves walk ONE shared K/V stream (key
-tiles 0 .. T0-1, double-buffered LDS images filled by LDS-DMA, exactly the
-W4 images).  Causal launches pair a heavy block X0 = nqb-1-i with a light
-one X1 = i of the same head, so every workgroup costs nqb+1 key tiles of 64
-rows (the reference's heaviest-first order, flash_attention.cu:103-112,
-taken to its balanced end), and a launch of B*H*S/128 rows fills the chip at
-S = 1024 (B=1, H=32: 256 workgroups) where 256-row items (W4) leave half of
-it idle and the 128-row KV-pair's heaviest block is 8/4.5 of the mean.
+per SIMD, on up to FOUR 64-row query blocks X0..X3 of one head (sorted by key
+tile count T0 >= T1 >= T2 >= T3; an absent block has T = 0).  Wave w holds 16
+rows of each -- row block b = rows 64 X_b + 16 w + r16 -- and the four waves
+walk ONE shared K/V stream (key tiles 0 .. T0-1, double-buffered LDS images
+filled by LDS-DMA, exactly the W4 images).  Causal launches group the heavy
+block nqb-1-r with the light block r of the same head (a pair), one or two
+pairs per workgroup, so every workgroup walks the same number of 64x64 tile
+products (the reference's heaviest-first order, flash_attention.cu:103-112,
+taken to its balanced end).  A launch of B*H*S query rows then fills the chip
+at 128 rows per workgroup (pairs: B=1 H=32 S=1024 is 256 workgroups, where
+W4's 256-row items leave half of it idle) and keeps 4 blocks per wave for as
+many tiles as possible at 256 (quads).
 
-Per key tile j (after the prologue computed S(0)) a wave runs, with NB = the
-row blocks still active (2 while the light block lasts, then 1):
-  phase A: QK^T(j+1), 16 NB MFMAs in 4 NB four-deep chains, beside the fp16
-           conversion of P(j), the running maxima of S(j+1), the K fragment
-           reads (each feeds NB MFMAs) and the LDS-DMA of K(j+2) / V(j+1)
-  phase B: PV(j) + row sums, 18 NB MFMAs, beside the rescale decision and
+Per key tile j (after the prologue computed S(0)) a wave runs, with NP = the
+blocks that have tile j (PV(j)) and NQ = those that have tile j+1 (QK^T(j+1)):
+  phase A: QK^T(j+1), 16 NQ MFMAs in 4 NQ four-deep chains, beside the fp16
+           conversion of P(j) of the NP blocks, the running maxima of S(j+1),
+           the K fragment reads (each feeds NQ MFMAs) and the LDS-DMA of
+           K(j+2) / V(j+1)
+  mask:    the blocks whose tile j+1 is their last (T_b = j+2): the limit
+           mask (causal diagonal / ragged end), then their maxima again
+  phase B: PV(j) + row sums, 18 NP MFMAs, beside the rescale decision and
            exp2 of S(j+1) and the V^T transposed reads
   s_waitcnt vmcnt(0), one barrier.
-Tiles that end a block run their own interleaved kinds (KINDS): a block's
-last tile (causal diagonal or ragged end) takes QK^T without the running
-maxima, then the limit mask and the maxima, then PV with the decision ahead
-of its first MFMA; a block's PV drain runs beside the other block's QK^T.
+A kind per (NP, NQ): steady (NQ = NP), one block's PV drain (NQ = NP - 1),
+all blocks' drain (NQ = 0).
 
 The arithmetic is M16's (fa_fwd_kernel.hpp) with the rescale decision per
 16-row block, checked against the oracle (reference cpu_attention) at the
@@ -39,6 +42,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import gen_w4_item as w4  # noqa: E402
 from gen_w4_item import DT, NINF, R, Stream, dsr, mfma, salu, set_dtype, valu, vmem  # noqa: E402
 
+NB = 4                 # query blocks per workgroup (at most)
 NT, NE = 4, 8          # head_dim 128: k-steps of a QK^T chain, 16-column O blocks
 ROWB = 256             # bytes of a Q/K/V/O row
 TILEB = 64 * ROWB      # a 64-key K or V tile
@@ -46,7 +50,7 @@ PASSL = 4096           # LDS stride of a staging pass
 RESCALE = "0x41000000"  # 8.0: m_ref moves when a row max grew past it (log2 units)
 
 # ---------------------------------------------------------------------------
-# register map (VGPR v0-v165, AGPR a0-a135; the compiler keeps the rest)
+# register map (VGPR v0-v213, AGPR a0-a239; the compiler keeps the rest)
 # ---------------------------------------------------------------------------
 
 
@@ -56,41 +60,41 @@ def S(b, cb, i=None):      # S^T tile: block b, 16-key block cb (fp32, exp2'd in
 
 
 def P(b, u, r=None):       # P fp16, B operand of PV: block b, 32-key step u
-    base = 32 + 8 * b + 4 * u
+    base = 64 + 8 * b + 4 * u
     return R("v", base, 4) if r is None else R("v", base + r)
 
 
 def NEGM(b, i=None):       # -m_ref broadcast: C operand of the first MFMA of a chain
-    return R("v", 48 + 4 * b, 4) if i is None else R("v", 48 + 4 * b + i)
+    return R("v", 96 + 4 * b, 4) if i is None else R("v", 96 + 4 * b + i)
 
 
 def KF(slot):              # K fragments: 8 slots (two 16-key blocks)
-    return R("v", 56 + 4 * slot, 4)
+    return R("v", 112 + 4 * slot, 4)
 
 
 def VF(slot, half=None):   # V^T fragments: 8 slots
-    base = 88 + 4 * slot
+    base = 144 + 4 * slot
     return R("v", base, 4) if half is None else R("v", base + 2 * half, 2)
 
 
 def KD(i):                 # per-pass LDS-DMA source offsets
-    return R("v", 120 + i)
+    return R("v", 176 + i)
 
 
 def VD(i):
-    return R("v", 124 + i)
+    return R("v", 180 + i)
 
 
-ONES = R("v", 128, 4)
-MREF = [R("v", 132), R("v", 133)]
-RMAX = [R("v", 134), R("v", 135)]            # running partial maxima per block
-VNINF = R("v", 136)
-T = [R("v", 137 + i) for i in range(11)]     # v137-v147 temporaries
-KOFF = ["%[koff]"] + [R("v", 148 + i) for i in range(3)]
-VOFF = ["%[voff]"] + [R("v", 151 + i) for i in range(3)]
-EPI = [f"v{154 + i}" for i in range(8)]      # epilogue staging
-XY = ["v162", "v163", "v164", "v165"]        # one store: X = v162,163 ; Y = v164,165
-NV = 166
+ONES = R("v", 184, 4)
+MREF = [R("v", 188 + b) for b in range(NB)]
+RMAX = [R("v", 192 + b) for b in range(NB)]   # running partial maxima per block
+VNINF = R("v", 196)
+T = [R("v", 197 + i) for i in range(11)]      # v197-v207 temporaries
+KOFF = ["%[koff]"] + [R("v", 208 + i) for i in range(3)]
+VOFF = ["%[voff]"] + [R("v", 211 + i) for i in range(3)]
+EPI = [f"v{144 + i}" for i in range(8)]       # epilogue staging (the free V^T slots)
+XY = ["v152", "v153", "v154", "v155"]         # one store: X = v152,153 ; Y = v154,155
+NV = 214
 
 
 def O(b, e, i=None):       # O^T accumulator, block b, d-block e
@@ -99,22 +103,22 @@ def O(b, e, i=None):       # O^T accumulator, block b, d-block e
 
 
 def L(b, i=None):          # row sums l
-    return R("a", 64 + 4 * b, 4) if i is None else R("a", 64 + 4 * b + i)
+    return R("a", 128 + 4 * b, 4) if i is None else R("a", 128 + 4 * b + i)
 
 
 def Q(b, t):               # Q * c (fp16), B operand of QK^T
-    return R("a", 72 + 16 * b + 4 * t, 4)
+    return R("a", 144 + 16 * b + 4 * t, 4)
 
 
 def KST1(i):               # prologue staging: K(1) / V(0)
-    return R("a", 104 + 4 * i, 4)
+    return R("a", 208 + 4 * i, 4)
 
 
 def VST1(i):
-    return R("a", 120 + 4 * i, 4)
+    return R("a", 224 + 4 * i, 4)
 
 
-NA = 136
+NA = 240
 
 # LDS images (W4's): K at 0 / 16384, V at 32768 / 49152
 KBUF = [0, 16384]
@@ -128,29 +132,34 @@ SKREM, SVREM = "s48", "s49"
 SJ, SJ1 = "s50", "s51"
 ST0, ST1 = "s52", "s53"
 KV0 = "s54"
+SNP = "s55"
 RQ, RO = "s[56:59]", "s[60:63]"
 SM0 = "s64"
 DIVS = "s[66:67]"
+SJ2 = "s68"
+STMP = "s69"
 NS_LO, NS_HI = 40, 72
 
-# block b's row base (64 X_b + 16 w), key bound, of the C++ side
-QR = ["%[qr0]", "%[qr1]"]
-KVH = ["%[kvh0]", "%[kvh1]"]
+# block b's row base (64 X_b + 16 w), key bound, key tiles, of the C++ side
+QR = [f"%[qr{b}]" for b in range(NB)]
+KVH = [f"%[kvh{b}]" for b in range(NB)]
+TB = [f"%[t{b}]" for b in range(NB)]
 
 MAX_OFF, LEFT_OFF, DEC_GAP = 2, 3, 6
 LAG = 2
 
 # diagnostic builds only (never the product library; tools/w4_variant.sh):
 # W4P_DIAG=stamps accumulates per wave the shader cycles of the prologue, of
-# each iteration kind (steady 2 blocks / steady 1 block / generic) with their
-# counts, of the end-of-iteration DMA wait + barrier and of the epilogue, and
-# stores them over O[qr0][0:16] (every lane the same 64 bytes)
+# the iterations with 4 / 3 / 2 / 1 blocks with a QK^T (steady or not), of
+# the drains (no QK^T), their counts, the end-of-iteration DMA wait + barrier
+# and the epilogue, and stores them over O[qr0][0:32] (every lane the same
+# 64 bytes)
 DIAG = os.environ.get("W4P_DIAG", "")
 STAMPS = DIAG == "stamps"
-# accumulators: s72 start, s74 path, s76 stamp, s78 s2, s79 s1, s80 gen,
-# s81 n_s2, s82 n_s1, s83 n_gen, s84 wait+barrier, s85 prologue, s86 epilogue
-# ("gen" = every iteration kind that ends a block: diagonal / ragged tile, drain)
-NS_DIAG = 88
+# s72 start, s74 path, s76 stamp, s78-s82 cycles of paths 0-4, s83-s87
+# counts, s88 wait+barrier, s89 prologue, s90 epilogue, s91 select tmp
+NS_DIAG = 92
+NPATH = 5
 
 
 def stamp_now(st, dst):
@@ -173,18 +182,18 @@ def stamp_path_end(st):
         return
     stamp_now(st, 76)
     st.raw("s_sub_u32 s75, s76, s72")
-    for k in range(3):
+    for k in range(NPATH):
         st.raw(f"s_cmp_eq_u32 s74, {k}")
         st.raw("s_cselect_b32 s77, s75, 0")
-        st.raw("s_cselect_b32 s87, 1, 0")
+        st.raw("s_cselect_b32 s91, 1, 0")
         st.raw(f"s_add_u32 s{78 + k}, s{78 + k}, s77")
-        st.raw(f"s_add_u32 s{81 + k}, s{81 + k}, s87")
+        st.raw(f"s_add_u32 s{83 + k}, s{83 + k}, s91")
 
 
-def vahead(nb):
-    """V^T fragments read ahead of their PV MFMAs: 8 (nb = 2) / 6 (nb = 1)
-    MFMAs of cover for the LDS latency"""
-    return 4 if nb == 2 else 6
+def vahead(np_):
+    """V^T fragments read ahead of their PV MFMAs: >= 8 MFMAs of cover for the
+    LDS latency"""
+    return {1: 6, 2: 4}.get(np_, 3)
 
 
 def kslot(cb, t):
@@ -214,7 +223,7 @@ def qk_chain(b, cb):
 
 
 def cvt_block(b, cb):
-    p = 32 + 8 * b + 4 * (cb >> 1) + 2 * (cb & 1)
+    p = 64 + 8 * b + 4 * (cb >> 1) + 2 * (cb & 1)
     s = 16 * b + 4 * cb
     return [valu(f"{DT['cvt_pk']} v{p}, v{s}, v{s + 1}", r=[f"v{s}", f"v{s + 1}"], w=[f"v{p}"]),
             valu(f"{DT['cvt_pk']} v{p + 1}, v{s + 2}, v{s + 3}", r=[f"v{s + 2}", f"v{s + 3}"], w=[f"v{p + 1}"])]
@@ -235,15 +244,15 @@ def exp_ops(b):
             for x in range(16 * b, 16 * b + 16)]
 
 
-def pv_mfmas(blocks):
-    """PV + row sums of `blocks`: for u: for e: the blocks; then their row sums"""
+def pv_mfmas(np_):
+    """PV + row sums of blocks 0..np-1: for u: for e: the blocks; then their row sums"""
     ms, frag_first = [], {}
     for u in range(2):
         for e in range(NE):
             frag_first[u * NE + e] = len(ms)
-            for b in blocks:
+            for b in range(np_):
                 ms.append(mfma(O(b, e), VF((u * NE + e) % 8), P(b, u), O(b, e)))
-        ms += [mfma(L(b), ONES, P(b, u), L(b)) for b in blocks]
+        ms += [mfma(L(b), ONES, P(b, u), L(b)) for b in range(np_)]
     return ms, frag_first
 
 
@@ -265,18 +274,18 @@ def dma_pieces(p):
 
 
 # ---------------------------------------------------------------------------
-# the steady iteration: phase A / phase B interleaved
+# one iteration: phase A / mask / phase B
 # ---------------------------------------------------------------------------
-def phase_a(st, p, qk, cvt, pv, with_max=True, dma=True):
-    """QK^T(j+1) of the blocks `qk` from kbuf[1-p] beside the fp16 conversion
-    of P(j) of the blocks `cvt` (each just before the chain that overwrites
-    its scores), the maxima of S(j+1) (with_max), the K reads, the stage's
-    LDS-DMA and the first V^T fragments of PV(j) of the blocks `pv`.  No qk
-    (the drain): the conversions and V^T reads alone."""
+def phase_a(st, p, nq, np_):
+    """QK^T(j+1) of blocks 0..nq-1 from kbuf[1-p] beside the fp16 conversion of
+    P(j) of blocks 0..np-1 (each just before the chain that overwrites its
+    scores), the running maxima of S(j+1), the K reads, the stage's LDS-DMA
+    and the first V^T fragments of PV(j).  nq = 0 (the last tile): the
+    conversions and V^T reads alone."""
     kb = KBUF[1 - p]
-    va = vahead(len(pv))
-    if not qk:
-        for b in cvt:
+    va = vahead(np_)
+    if nq == 0:
+        for b in range(np_):
             for cb in range(4):
                 for c in cvt_block(b, cb):
                     st.emit(c)
@@ -284,7 +293,7 @@ def phase_a(st, p, qk, cvt, pv, with_max=True, dma=True):
             for r in v_reads(f, VBUF[p]):
                 st.emit(r)
         return []
-    chains = [(b, cb) for cb in range(4) for b in qk]
+    chains = [(b, cb) for cb in range(4) for b in range(nq)]
     mf = []
     for b, cb in chains:
         mf += qk_chain(b, cb)
@@ -296,36 +305,34 @@ def phase_a(st, p, qk, cvt, pv, with_max=True, dma=True):
 
     put(0, [k_read(t, 0, kb) for t in range(NT)])
     for x, (b, cb) in enumerate(chains):
-        if b in cvt:
-            c = cvt_block(b, cb)
-            if cb == 0:
-                put(0, c)
-            else:
-                put(NT * x - 1, c[0])
-                put(NT * x, c[1])
-        if b == qk[0] and cb < 3:
+        c = cvt_block(b, cb)
+        if cb == 0:
+            put(0, c)
+        else:
+            put(NT * x - 1, c[0])
+            put(NT * x, c[1])
+        if b == 0 and cb < 3:
             for t in range(NT):
                 put(NT * x + 1 + t % 3, k_read(t, cb + 1, kb))
-        if with_max and x >= LAG:
+        if x >= LAG:
             by, cby = chains[x - LAG]
             mm = max_block(by, cby, first=(cby == 0))
             put(NT * x + MAX_OFF, mm[0])
             put(min(NT * x + MAX_OFF + 1, n), mm[1])
-    # conversions of a block with a PV(j) but no QK(j+1) (its drain): any gap
-    extra = [c for b in cvt if b not in qk for cb in range(4) for c in cvt_block(b, cb)]
+    # conversions of the blocks with a PV(j) but no QK(j+1) (their drain): any gap
+    extra = [c for b in range(nq, np_) for cb in range(4) for c in cvt_block(b, cb)]
     for i, c in enumerate(extra):
         put(1 + (i * (n - 2)) // len(extra), c)
-    if dma:
-        # LDS-DMA: an M0 write and its load are always an MFMA apart (M0 wait
-        # state); two blocks spread them over two gaps each, one shares gaps
-        pairs, adv = dma_pieces(p)
-        a0, sp = (2, 2) if len(qk) == 2 else (1, 1)
-        for i, (m0, ld) in enumerate(pairs):
-            put(a0 + sp * i, m0)
-            put(a0 + sp * i + 1, ld)
-        g = a0 + sp * (len(pairs) - 1) + 2
-        for i, ins in enumerate(adv):
-            put(g + i, ins)
+    # LDS-DMA: an M0 write and its load are always an MFMA apart (M0 wait
+    # state); two or more blocks spread them over two gaps each, one shares gaps
+    pairs, adv = dma_pieces(p)
+    a0, sp = (2, 2) if nq >= 2 else (1, 1)
+    for i, (m0, ld) in enumerate(pairs):
+        put(a0 + sp * i, m0)
+        put(a0 + sp * i + 1, ld)
+    g = a0 + sp * (len(pairs) - 1) + 2
+    for i, ins in enumerate(adv):
+        put(g + i, ins)
     # the first V^T fragments of PV(j) (V(j) is ready since the last barrier)
     for f in range(va):
         for i, r in enumerate(v_reads(f, VBUF[p])):
@@ -333,11 +340,105 @@ def phase_a(st, p, qk, cvt, pv, with_max=True, dma=True):
     assert max(gaps) <= n, "every filler lands in a gap"
     st.interleave(mf, gaps)
     left = []
-    if with_max:
-        for y in range(len(chains) - LAG, len(chains)):
-            by, cby = chains[y]
-            left += max_block(by, cby, first=False)
+    for y in range(len(chains) - LAG, len(chains)):
+        by, cby = chains[y]
+        left += max_block(by, cby, first=False)
     return left
+
+
+def mask_pass(st, nq, causal):
+    """blocks 0..nq-1 whose tile j+1 is their last (T_b = j+2): the limit mask,
+    then their running maxima again (over the masked scores; phase B's
+    leftover maxima re-max the masked values, a no-op).  T is sorted
+    descending and every QK block has T_b >= j+2, so none is masked unless
+    the last one is: one compare in the common case."""
+    if nq == 0:
+        return
+    done = w4.newlabel("nomask")
+    st.raw(f"s_cmp_eq_u32 {TB[nq - 1]}, {SJ2}")
+    st.branch("s_cbranch_scc0", done)
+    st.raw(f"s_lshl_b32 {KV0}, {SJ1}, 6")
+    for b in range(nq):
+        skip = w4.newlabel(f"nomask{b}_")
+        if b < nq - 1:
+            st.raw(f"s_cmp_eq_u32 {TB[b]}, {SJ2}")
+            st.branch("s_cbranch_scc0", skip)
+        mask_block(st, b, causal)
+        full_max(st, b)
+        st.label(skip)
+    st.label(done)
+
+
+def phase_b(st, p, nq, np_, leftover, label_slow, label_end):
+    """PV(j) of blocks 0..np-1 from vbuf[p]; the rescale decision over the
+    blocks 0..nq-1 at DEC_GAP, exp2 of their S(j+1) after it.  nq = 0: the
+    PV alone."""
+    vb = VBUF[p]
+    mf, frag_first = pv_mfmas(np_)
+    n = len(mf)
+    gaps = {}
+
+    def put(k, ins):
+        gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
+
+    va = vahead(np_)
+    for f in range(va, 2 * NE):
+        k = frag_first[f - va]
+        r = v_reads(f, vb)
+        put(k + 1, r[0])
+        put(k + 2, r[1])
+    for i, ins in enumerate(leftover):
+        put(LEFT_OFF + i, ins)
+    assert not leftover or LEFT_OFF + len(leftover) - 1 <= DEC_GAP
+    if nq == 0:
+        st.interleave(mf, gaps)
+        st.branch("s_branch", label_end)
+        return
+    m = RMAX[0]
+    dec = []
+    if nq >= 2:
+        m = T[0]
+        dec.append(valu(f"v_max3_f32 {T[0]}, {RMAX[0]}, {RMAX[1]}, {RMAX[2 if nq > 2 else 1]}",
+                        r=RMAX[:nq], w=[T[0]]))
+        if nq == 4:
+            dec.append(valu(f"v_max_f32 {T[0]}, {T[0]}, {RMAX[3]}", r=[T[0], RMAX[3]], w=[T[0]]))
+    dec.append(valu(f"v_cmp_lt_f32 vcc, {RESCALE}, {m}", r=[m]))
+    exs = [e for b in range(nq) for e in exp_ops(b)]
+    n_g = n - DEC_GAP
+    for i, e in enumerate(exs):
+        put(DEC_GAP + 1 + (i * n_g) // len(exs), e)
+    for k in range(DEC_GAP):
+        for f in gaps.get(k, []):
+            st.emit(f)
+        st.emit(mf[k])
+    for f in gaps.get(DEC_GAP, []):
+        st.emit(f)
+    for d in dec:
+        st.emit(d)
+    st.branch("s_cbranch_vccnz", label_slow)
+    for k in range(DEC_GAP, n):
+        if k > DEC_GAP:
+            for f in gaps.get(k, []):
+                st.emit(f)
+        st.emit(mf[k])
+    for f in gaps.get(n, []):
+        st.emit(f)
+    st.branch("s_branch", label_end)
+    # slow path: the remaining PV MFMAs (their V reads, no exps), then rescale
+    st.label(label_slow)
+    for k in range(DEC_GAP, n):
+        if k > DEC_GAP:
+            for f in gaps.get(k, []):
+                if isinstance(f, str) or f.kind != "trans":
+                    st.emit(f)
+        st.emit(mf[k])
+    for f in gaps.get(n, []):
+        if isinstance(f, str) or f.kind != "trans":
+            st.emit(f)
+    slow_softmax(st, range(nq), first=False)
+    for e in exs:
+        st.emit(e)
+    st.branch("s_branch", label_end)
 
 
 def slow_softmax(st, blocks, first):
@@ -393,77 +494,6 @@ def shift_block(st, b, sh, first):
         st.emit(valu(f"v_xor_b32 {NEGM(b, i)}, 0x80000000, {MREF[b]}", r=[MREF[b]], w=[NEGM(b, i)]))
 
 
-def phase_b(st, p, pv, ex, leftover, dec_gap, label_slow, label_end):
-    """PV(j) of the blocks `pv` from vbuf[p]; the rescale decision over the
-    blocks `ex` (those with a QK(j+1)) at dec_gap, exp2 of their S(j+1)
-    after it.  No ex (the drain): the PV alone."""
-    vb = VBUF[p]
-    mf, frag_first = pv_mfmas(pv)
-    n = len(mf)
-    gaps = {}
-
-    def put(k, ins):
-        gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
-
-    va = vahead(len(pv))
-    for f in range(va, 2 * NE):
-        k = frag_first[f - va]
-        r = v_reads(f, vb)
-        put(k + 1, r[0])
-        put(k + 2, r[1])
-    for i, ins in enumerate(leftover):
-        put(LEFT_OFF + i, ins)
-    assert not leftover or LEFT_OFF + len(leftover) - 1 <= dec_gap
-    if not ex:
-        st.interleave(mf, gaps)
-        st.branch("s_branch", label_end)
-        return
-    if len(ex) == 2:
-        dec = [valu(f"v_max_f32 {T[0]}, {RMAX[0]}, {RMAX[1]}", r=RMAX, w=[T[0]]),
-               valu(f"v_cmp_lt_f32 vcc, {RESCALE}, {T[0]}", r=[T[0]])]
-    else:
-        dec = [valu(f"v_cmp_lt_f32 vcc, {RESCALE}, {RMAX[ex[0]]}", r=[RMAX[ex[0]]])]
-    exs = [e for b in ex for e in exp_ops(b)]
-    n_g = n - dec_gap
-    for i, e in enumerate(exs):
-        put(dec_gap + 1 + (i * n_g) // len(exs), e)
-    for k in range(dec_gap):
-        for f in gaps.get(k, []):
-            st.emit(f)
-        st.emit(mf[k])
-    for f in gaps.get(dec_gap, []):
-        st.emit(f)
-    for d in dec:
-        st.emit(d)
-    st.branch("s_cbranch_vccnz", label_slow)
-    for k in range(dec_gap, n):
-        if k > dec_gap:
-            for f in gaps.get(k, []):
-                st.emit(f)
-        st.emit(mf[k])
-    for f in gaps.get(n, []):
-        st.emit(f)
-    st.branch("s_branch", label_end)
-    # slow path: the remaining PV MFMAs (their V reads, no exps), then rescale
-    st.label(label_slow)
-    for k in range(dec_gap, n):
-        if k > dec_gap:
-            for f in gaps.get(k, []):
-                if isinstance(f, str) or f.kind != "trans":
-                    st.emit(f)
-        st.emit(mf[k])
-    for f in gaps.get(n, []):
-        if isinstance(f, str) or f.kind != "trans":
-            st.emit(f)
-    slow_softmax(st, ex, first=False)
-    for e in exs:
-        st.emit(e)
-    st.branch("s_branch", label_end)
-
-
-# ---------------------------------------------------------------------------
-# iteration kinds
-# ---------------------------------------------------------------------------
 def mask_block(st, b, causal):
     """S(b) = -inf where key >= kv_hi_b or (causal) key > query row, for the
     tile at key KV0 (key kv = KV0 + 16cb + 4sg + i, row = qr_b + r16):
@@ -493,53 +523,34 @@ def full_max(st, b):
             st.emit(ins)
 
 
-def qk_plain(st, kb, blocks):
-    """QK^T of one tile for `blocks`, not interleaved (prologue): per 16-key
-    block its four K fragments were read one block ahead"""
+def qk_plain(st, kb, nb):
+    """QK^T of one tile for blocks 0..nb-1, not interleaved (prologue): each
+    16-key block's four K fragments read one block ahead"""
     for t in range(NT):
         st.emit(k_read(t, 0, kb))
     for cb in range(4):
         if cb < 3:
             for t in range(NT):
                 st.emit(k_read(t, cb + 1, kb))
-        for b in blocks:
+        for b in range(nb):
             for m in qk_chain(b, cb):
                 st.emit(m)
 
 
-# iteration kinds: (qk blocks, blocks with P(j) / PV(j), blocks whose QK(j+1)
-# tile is their last -- masked --); steady kinds have no mask
-KINDS = {
-    "s2": ((0, 1), (0, 1), ()),    # both blocks in their key range
-    "s1": ((0,), (0,), ()),        # block 0 alone (block 1 done / absent)
-    "A": ((0, 1), (0, 1), (1,)),   # block 1's last tile (causal diagonal)
-    "A2": ((0, 1), (0, 1), (0, 1)),  # both blocks' last tile (non-causal pair)
-    "B": ((0,), (0, 1), ()),       # block 1's PV drain beside block 0's QK
-    "B2": ((0,), (0, 1), (0,)),    # ... and block 0's last tile
-    "C": ((0,), (0,), (0,)),       # block 0's last tile
-    "D": ((), (0,), ()),           # block 0's PV drain
-    "D2": ((), (0, 1), ()),        # both blocks' PV drain
-}
+# iteration kinds (NP, NQ): steady, one block's drain, every block's drain
+KINDS = [(k, k) for k in range(1, NB + 1)] + [(k, k - 1) for k in range(1, NB + 1)] + \
+        [(k, 0) for k in range(2, NB + 1)]
 
 
-def iteration(st, p, kind, causal, Lb):
-    qk, pv, masked = KINDS[kind]
-    stamp_path(st, {"s2": 0, "s1": 1}.get(kind, 2))
-    slow = Lb["slow_" + kind][p]
-    if not masked:
-        left = phase_a(st, p, list(qk), list(pv), list(pv), with_max=True, dma=bool(qk))
-        phase_b(st, p, list(pv), list(qk), left, DEC_GAP if qk else 0, slow, Lb["end"][p])
-        return
-    # a block's last tile: QK^T without the running maxima, the limit mask on
-    # the blocks whose tile it is, the maxima of every QK block, then PV with
-    # the decision ahead of its first MFMA (gen_w4_item's general path)
-    phase_a(st, p, list(qk), list(pv), list(pv), with_max=False, dma=True)
-    st.raw(f"s_lshl_b32 {KV0}, {SJ1}, 6")
-    for b in masked:
-        mask_block(st, b, causal)
-    for b in qk:
-        full_max(st, b)
-    phase_b(st, p, list(pv), list(qk), [], 0, slow, Lb["end"][p])
+def kname(np_, nq):
+    return f"k{np_}{nq}"
+
+
+def iteration(st, p, np_, nq, causal, Lb):
+    stamp_path(st, NB - nq if nq else NPATH - 1)   # 0: 4 QK blocks .. 3: 1; 4: drain
+    left = phase_a(st, p, nq, np_)
+    mask_pass(st, nq, causal)
+    phase_b(st, p, nq, np_, left, Lb["slow_" + kname(np_, nq)][p], Lb["end"][p])
 
 
 # ---------------------------------------------------------------------------
@@ -553,13 +564,13 @@ def rsrc(st, dst, lo, hi, records):
 
 
 def q_scale(st):
-    """Q * c (fp32 product rounded to fp16 once, M16::scale_q) from v0-31 into
-    a72-103, eight elements at a time in the (free) V^T fragment registers"""
-    for x0 in range(0, 32, 8):
+    """Q * c (fp32 product, then fp16: M16::scale_q) from v0-63 into a144-207,
+    eight elements at a time in the (free) V^T fragment registers"""
+    for x0 in range(0, 16 * NB, 8):
         xs = range(x0, x0 + 8)
-        lo = {x: f"v{88 + 3 * (x - x0)}" for x in xs}
-        hi = {x: f"v{89 + 3 * (x - x0)}" for x in xs}
-        pk = {x: f"v{90 + 3 * (x - x0)}" for x in xs}
+        lo = {x: f"v{144 + 3 * (x - x0)}" for x in xs}
+        hi = {x: f"v{145 + 3 * (x - x0)}" for x in xs}
+        pk = {x: f"v{146 + 3 * (x - x0)}" for x in xs}
         if DT["bf16"]:
             for x in xs:
                 st.raw(f"v_lshlrev_b32_e32 {lo[x]}, 16, v{x}")
@@ -574,12 +585,13 @@ def q_scale(st):
         for x in xs:
             st.raw(f"{DT['cvt_pk']} {pk[x]}, {lo[x]}, {hi[x]}")
         for x in xs:
-            st.raw(f"v_accvgpr_write_b32 a{72 + x}, {pk[x]}")
+            st.raw(f"v_accvgpr_write_b32 a{144 + x}, {pk[x]}")
 
 
 def prologue(st, causal):
-    """descriptors, Q (both blocks) / K(0) / V(0) / K(1) loads, Q scaling,
-    S(0) = K(0) Q^T with the tile-0 mask and the first-tile softmax"""
+    """descriptors, Q (every block) / K(0) / V(0) / K(1) loads, Q scaling,
+    S(0) = K(0) Q^T of the blocks with a tile, the tile-0 mask where it is a
+    block's last tile, the first-tile softmax"""
     if STAMPS:
         for r in range(72, NS_DIAG):
             st.raw(f"s_mov_b32 s{r}, 0")
@@ -597,19 +609,19 @@ def prologue(st, causal):
         st.raw(f"v_add_u32 {VOFF[i]}, {4096 * i}, %[voff]")
     st.raw(f"v_mov_b32 {VNINF}, {NINF}")
     for i in range(4):
-        st.raw(f"v_mov_b32 v{128 + i}, {DT['one2']}")
+        st.raw(f"v_mov_b32 v{184 + i}, {DT['one2']}")
     rsrc(st, 56, "%[qlo]", "%[qhi]", "%[qrec]")
     rsrc(st, 40, "%[klo]", "%[khi]", "%[kvrec]")
     rsrc(st, 44, "%[vlo]", "%[vhi]", "%[kvrec]")
     rsrc(st, 60, "%[olo]", "%[ohi]", "%[qrec]")
     # Q rows qr_b + r16, chunk g of k-step t: (qr_b << 8) + qoff + 64 t
-    for b in range(2):
+    for b in range(NB):
         st.raw(f"s_lshl_b32 {ST0}, {QR[b]}, 8")
         st.raw(f"v_add_u32 {T[b]}, {ST0}, %[qoff]")
     for i in range(4):
         st.raw(f"v_add_u32 {T[4 + i]}, {hex(TILEB)}, {KOFF[i]}")
-    st.nop(5)  # SALU-written descriptors -> buffer loads
-    for b in range(2):
+    st.nop(5)
+    for b in range(NB):
         for t in range(NT):
             st.raw(f"buffer_load_dwordx4 {R('v', 16 * b + 4 * t, 4)}, {T[b]}, {RQ}, 0 offen offset:{64 * t}")
     for i in range(4):
@@ -629,13 +641,13 @@ def prologue(st, causal):
     st.raw(f"s_sub_i32 {SVREM}, s46, {t1}")
     st.raw(f"s_max_i32 s46, {SVREM}, 0")
     # O, l, -m_ref, m_ref = 0
-    for x in range(72):
+    for x in range(144):
         st.raw(f"v_accvgpr_write_b32 a{x}, 0")
-    for x in range(48, 56):
+    for x in range(96, 112):
         st.raw(f"v_mov_b32 v{x}, 0")
-    for b in range(2):
+    for b in range(NB):
         st.raw(f"v_mov_b32 {MREF[b]}, 0")
-    # Q (8) and K(0) (4) landed; V(0), K(1) (8) may still fly
+    # Q (16) and K(0) (4) landed; V(0), K(1) (8) may still fly
     st.raw("s_waitcnt vmcnt(8)")
     for i in range(4):
         st.raw(f"ds_write_b128 %[klds], {KF(i)} offset:{KBUF[0] + PASSL * i}")
@@ -647,38 +659,47 @@ def prologue(st, causal):
     st.raw("s_waitcnt lgkmcnt(0)")
     st.raw("s_barrier")
     st.nop(2)
-    # S(0): block 1 only if the item has one
-    one, s0done = w4.newlabel("s0one"), w4.newlabel("s0done")
-    st.raw("s_cmp_eq_u32 %[tl], 0")
-    st.branch("s_cbranch_scc1", one)
-    qk_plain(st, KBUF[0], [0, 1])
-    st.branch("s_branch", s0done)
-    st.label(one)
-    qk_plain(st, KBUF[0], [0])
+    # S(0) of the blocks with a tile (a prefix: T sorted descending)
+    s0done = w4.newlabel("s0done")
+    lbl = {nb: w4.newlabel(f"s0n{nb}") for nb in range(1, NB + 1)}
+    for nb in range(NB, 1, -1):
+        st.raw(f"s_cmp_lg_u32 {TB[nb - 1]}, 0")
+        st.branch("s_cbranch_scc1", lbl[nb])
+    st.branch("s_branch", lbl[1])
+    for nb in range(NB, 0, -1):
+        st.label(lbl[nb])
+        qk_plain(st, KBUF[0], nb)
+        st.branch("s_branch", s0done)
     st.label(s0done)
     st.raw(f"s_mov_b32 {KV0}, 0")
-    blk1 = w4.newlabel("first1")
-    for b in range(2):
-        if b == 1:
-            st.raw("s_cmp_eq_u32 %[tl], 0")
-            st.branch("s_cbranch_scc1", blk1)
+    first_done = w4.newlabel("firstdone")
+    for b in range(NB):
+        if b > 0:
+            st.raw(f"s_cmp_eq_u32 {TB[b]}, 0")
+            st.branch("s_cbranch_scc1", first_done)
         # tile 0 needs the limit mask only when it is the block's last tile
-        nomask = w4.newlabel(f"nomask{b}")
-        st.raw(f"s_cmp_eq_u32 {'%[th]' if b == 0 else '%[tl]'}, 1")
+        nomask = w4.newlabel(f"nomask0_{b}")
+        st.raw(f"s_cmp_eq_u32 {TB[b]}, 1")
         st.branch("s_cbranch_scc0", nomask)
         mask_block(st, b, causal)
         st.label(nomask)
         slow_softmax(st, [b], first=True)
         for e in exp_ops(b):
             st.emit(e)
-    st.label(blk1)
+    st.label(first_done)
     # every wave's S(0) K reads are done before iteration 0's DMA refills kbuf[0]
     st.lgkm_all()
     st.raw("s_barrier")
     st.raw(f"s_mov_b32 {SJ}, 0")
+    # NP of iteration 0: the blocks with a tile
+    st.raw(f"s_mov_b32 {SNP}, 0")
+    for b in range(NB):
+        st.raw(f"s_cmp_lg_u32 {TB[b]}, 0")
+        st.raw(f"s_cselect_b32 {STMP}, 1, 0")
+        st.raw(f"s_add_u32 {SNP}, {SNP}, {STMP}")
     if STAMPS:
         stamp_now(st, 72)
-        st.raw("s_sub_u32 s85, s72, s76")
+        st.raw("s_sub_u32 s89, s72, s76")
 
 
 def epilogue_block(st, b):
@@ -718,44 +739,38 @@ def epilogue_block(st, b):
         st.emit(valu(f"{DT['cvt_pk']} {Y[1]}, {EPI[6]}, {EPI[7]}", r=EPI[6:8], w=[Y[1]]))
         for dw in range(2):
             st.emit(valu(f"v_permlane16_swap_b32 {X[dw]}, {Y[dw]}", r=[X[dw], Y[dw]], w=[X[dw], Y[dw]]))
-        st.emit(vmem(f"buffer_store_dwordx4 v[162:165], {T[7]}, {RO}, 0 offen offset:{64 * ep} sc1",
-                     r=["v[162:165]", T[7]]))
+        st.emit(vmem(f"buffer_store_dwordx4 v[152:155], {T[7]}, {RO}, 0 offen offset:{64 * ep} sc1",
+                     r=["v[152:155]", T[7]]))
     st.nop(2)
 
 
 # ---------------------------------------------------------------------------
 def body(st, p, causal, Lb):
-    """iteration j (parity p = j & 1), one of KINDS by where j stands against
-    T0 = %[th] and T1 = %[tl] (T1 <= T0; T1 = 0: no block 1); then the
-    stage's DMA wait and the barrier"""
-    K = lambda k: Lb["k_" + k][p]  # noqa: E731
+    """iteration j (parity p = j & 1): the kind of (NP, NQ) = (#{T_b > j},
+    #{T_b > j+1}) -- NP carried from the previous iteration's NQ, NQ = NP
+    unless block NP-1 ends at tile j (then NP-1, or 0 when every block does:
+    equal tile counts) -- then the stage's DMA wait and the barrier"""
+    K = lambda np_, nq: Lb["k_" + kname(np_, nq)][p]  # noqa: E731
     st.label(Lb["loop"][p], drain_lgkm=True)
     st.raw(f"s_add_u32 {SJ1}, {SJ}, 1")
-    st.raw(f"s_add_u32 {ST0}, {SJ}, 2")
-    st.raw(f"s_cmp_lt_u32 {ST0}, %[tl]")       # j+2 < T1: both steady
-    st.branch("s_cbranch_scc1", K("s2"))
-    st.raw(f"s_cmp_eq_u32 {ST0}, %[tl]")       # j+2 == T1: block 1's last tile
-    st.branch("s_cbranch_scc0", Lb["d1"][p])
-    st.raw("s_cmp_eq_u32 %[tl], %[th]")
-    st.branch("s_cbranch_scc1", K("A2"))
-    st.branch("s_branch", K("A"))
-    st.label(Lb["d1"][p])
-    st.raw(f"s_cmp_eq_u32 {SJ1}, %[tl]")       # j+1 == T1: block 1's drain
-    st.branch("s_cbranch_scc0", Lb["d2"][p])
-    st.raw(f"s_cmp_lt_u32 {ST0}, %[th]")
-    st.branch("s_cbranch_scc1", K("B"))
-    st.raw(f"s_cmp_eq_u32 {ST0}, %[th]")
-    st.branch("s_cbranch_scc1", K("B2"))
-    st.branch("s_branch", K("D2"))
-    st.label(Lb["d2"][p])
-    st.raw(f"s_cmp_lt_u32 {ST0}, %[th]")       # j+2 < T0: block 0 steady alone
-    st.branch("s_cbranch_scc1", K("s1"))
-    st.raw(f"s_cmp_eq_u32 {ST0}, %[th]")
-    st.branch("s_cbranch_scc1", K("C"))
-    st.branch("s_branch", K("D"))
-    for kind in KINDS:
-        st.label(K(kind))
-        iteration(st, p, kind, causal, Lb)
+    st.raw(f"s_add_u32 {SJ2}, {SJ}, 2")
+    lbl = {k: w4.newlabel(f"np{k}_") for k in range(1, NB + 1)}
+    for k in range(NB, 1, -1):
+        st.raw(f"s_cmp_eq_u32 {SNP}, {k}")
+        st.branch("s_cbranch_scc1", lbl[k])
+    for k in range(1, NB + 1):
+        if k > 1:
+            st.label(lbl[k])
+        st.raw(f"s_cmp_gt_u32 {TB[k - 1]}, {SJ1}")   # block k-1 has tile j+1: steady
+        st.branch("s_cbranch_scc1", K(k, k))
+        if k > 1:
+            st.raw(f"s_cmp_eq_u32 {TB[0]}, {SJ1}")   # every block ends at tile j
+            st.branch("s_cbranch_scc1", K(k, 0))
+        st.branch("s_branch", K(k, k - 1))
+    for np_, nq in KINDS:
+        st.label(K(np_, nq))
+        st.raw(f"s_mov_b32 {SNP}, {nq}")             # NP of iteration j+1
+        iteration(st, p, np_, nq, causal, Lb)
     st.label(Lb["end"][p], drain_lgkm=True)
     stamp_path_end(st)
     st.raw("s_waitcnt vmcnt(0)")   # this iteration's LDS-DMA landed before the barrier publishes it
@@ -763,9 +778,9 @@ def body(st, p, causal, Lb):
     if STAMPS:
         stamp_now(st, 72)
         st.raw("s_sub_u32 s75, s72, s76")
-        st.raw("s_add_u32 s84, s84, s75")
+        st.raw("s_add_u32 s88, s88, s75")
     st.raw(f"s_add_u32 {SJ}, {SJ}, 1")
-    st.raw(f"s_cmp_lt_u32 {SJ}, %[th]")
+    st.raw(f"s_cmp_lt_u32 {SJ}, {TB[0]}")
     if p == 0:
         st.branch("s_cbranch_scc0", Lb["done"])
     else:
@@ -775,26 +790,29 @@ def body(st, p, causal, Lb):
 def generate(causal):
     st = Stream()
     Lb = {k: [w4.newlabel(f"{k}{p}") for p in range(2)]
-          for k in ["loop", "end", "d1", "d2"] + [f"k_{x}" for x in KINDS] + [f"slow_{x}" for x in KINDS]}
+          for k in ["loop", "end"] + [f"k_{kname(*x)}" for x in KINDS] + [f"slow_{kname(*x)}" for x in KINDS]}
     Lb["done"] = w4.newlabel("done")
     prologue(st, causal)
     body(st, 0, causal, Lb)
     body(st, 1, causal, Lb)
     st.label(Lb["done"], drain_lgkm=True)
     stamp_now(st, 76)
-    epilogue_block(st, 0)
-    nob1 = w4.newlabel("nob1")
-    st.raw("s_cmp_eq_u32 %[tl], 0")
-    st.branch("s_cbranch_scc1", nob1)
-    epilogue_block(st, 1)
-    st.label(nob1)
+    end = w4.newlabel("epidone")
+    for b in range(NB):
+        if b > 0:
+            st.raw(f"s_cmp_eq_u32 {TB[b]}, 0")
+            st.branch("s_cbranch_scc1", end)
+        epilogue_block(st, b)
+    st.label(end)
     if STAMPS:
         st.raw("s_waitcnt vmcnt(0)")
         stamp_now(st, 72)
-        st.raw("s_sub_u32 s86, s72, s76")
+        st.raw("s_sub_u32 s90, s72, s76")
         st.raw(f"s_lshl_b32 {ST1}, {QR[0]}, 8")
-        for i in range(16):
+        for i in range(13):
             st.raw(f"v_mov_b32 v{i}, s{78 + i}")
+        for i in range(13, 16):
+            st.raw(f"v_mov_b32 v{i}, 0")
         st.raw(f"v_mov_b32 v16, {ST1}")
         st.nop(2)
         for i in range(4):
@@ -805,8 +823,8 @@ def generate(causal):
 
 
 HEADER = """// GENERATED by gen_w4p_item.py -- do not edit.
-// One paired item (two 64-row query blocks x all key tiles) of the W4P tier:
-// see the generator's docstring for the register map and the schedule.
+// One multi-block item (up to four 64-row query blocks x all key tiles) of the
+// W4P tier: see the generator's docstring for the register map and the schedule.
 #pragma once
 """
 
@@ -817,6 +835,8 @@ def cxx(causal, bf16, lines):
     aclob = ", ".join(f'"a{i}"' for i in range(NA))
     sclob = ", ".join(f'"s{i}"' for i in range(NS_LO, NS_DIAG if STAMPS else NS_HI))
     name = ("w4p_item_causal" if causal else "w4p_item_noncausal") + ("_bf16" if bf16 else "_f16")
+    blocks = ",\n        ".join(f'[qr{b}] "s"(rn.qr[{b}]), [kvh{b}] "s"(rn.kvh[{b}]), [t{b}] "s"(rn.t[{b}])'
+                                 for b in range(NB))
     return f"""
 __device__ __forceinline__ void {name}(const W4PRun& rn, const W4Lane& ln) {{
   asm volatile(
@@ -824,8 +844,8 @@ __device__ __forceinline__ void {name}(const W4PRun& rn, const W4Lane& ln) {{
       :
       : [qlo] "s"(rn.qlo), [qhi] "s"(rn.qhi), [klo] "s"(rn.klo), [khi] "s"(rn.khi),
         [vlo] "s"(rn.vlo), [vhi] "s"(rn.vhi), [olo] "s"(rn.olo), [ohi] "s"(rn.ohi),
-        [qrec] "s"(rn.qrec), [kvrec] "s"(rn.kvrec), [qr0] "s"(rn.qr0), [qr1] "s"(rn.qr1),
-        [kvh0] "s"(rn.kvh0), [kvh1] "s"(rn.kvh1), [th] "s"(rn.th), [tl] "s"(rn.tl),
+        [qrec] "s"(rn.qrec), [kvrec] "s"(rn.kvrec),
+        {blocks},
         [c] "s"(rn.c), [dmab] "s"(rn.dmab),
         [ka0] "v"(ln.ka[0]), [ka1] "v"(ln.ka[1]), [ka2] "v"(ln.ka[2]), [ka3] "v"(ln.ka[3]),
         [va0] "v"(ln.va[0]), [va1] "v"(ln.va[1]), [koff] "v"(ln.koff), [voff] "v"(ln.voff),

@@ -18,7 +18,7 @@ for spec in $SHAPES; do
   spec=${spec//,/ }
   set -- $spec
   # the paired tier, the KV-pair, the KV-quad and the default dispatch (auto)
-  c=$(python -c "import sys; sys.path.insert(0, '.'); import fa_mi355x as fa; m = 'causal' if '$4' == '--causal' else 'noncausal'; print(','.join(str(next(c.id for c in fa.configs() if c.name == n + m)) for n in ('bm128_bn64_w4x32_m16_asm_pair_', 'bm128_bn64_w8_m16_kvpair_', 'bm64_bn64_w8_m16_kvquad_')))")
+  c=$(python -c "import sys; sys.path.insert(0, '.'); import fa_mi355x as fa; m = 'causal' if '$4' == '--causal' else 'noncausal'; print(','.join(str(next(c.id for c in fa.configs() if c.name == n + m)) for n in ${TIERS:-('bm128_bn64_w4x32_m16_asm_pair_', 'bm128_bn64_w8_m16_kvpair_', 'bm64_bn64_w8_m16_kvquad_')}))")
   timeout -k 10 120 python tools/ab.py --configs $c,auto --batch $1 --heads $2 --seq $3 $4 --rounds 5 --iters 20 \
     >> $out 2>&1 || { echo "ab failed: $spec"; tail -5 $out; exit 1; }
 done

@@ -89,7 +89,7 @@ def test_config_table():
         need = 2 * nbuf * c.block_n * 256
         if "_pingpong_persistent_" in c.name and "_dma_" not in c.name and not c.causal:
             need = max(need, KVPAIR_LDS)  # room for the KV-pair tail halves
-        if "_w4x64_" in c.name:
+        if "_w4x64_" in c.name and "_asm_quad_" not in c.name:
             need += 256 * 64  # the item table (256 slots of 16 dwords)
         assert c.lds_bytes == need <= 160 * 1024
     # every (waves, bn) non-split config exists for both masks
@@ -126,8 +126,9 @@ def test_select_config(causal):
         assert want in cfgs[fa.select_config(b, h, s, causal)].name, (b, h, s, causal)
     for b, h, s in ((1, 16, 2048), (1, 8, 4096), (2, 8, 2048)):  # <= 1 round of pairs
         assert "_asm_pair_" in cfgs[fa.select_config(b, h, s, causal)].name, (b, h, s, causal)
-    if causal:  # more than a round at S=4096: the KV-pair
-        assert "_kvpair_" in cfgs[fa.select_config(1, 12, 4096, True)].name
+    if causal:  # 1-2 rounds of pairs: two pairs per workgroup
+        for b, h, s in ((1, 32, 2048), (2, 32, 1024), (1, 16, 4096)):
+            assert "_asm_quad_" in cfgs[fa.select_config(b, h, s, True)].name, (b, h, s)
 
 
 def _null_call(lib, head_dim=128, b=1, h=1, s=64, causal=0, ptr=None):
@@ -257,6 +258,9 @@ def test_config_table_ships_only_used_tiers():
     # BN=128 (the reference's long non-causal tile, flash_attention.cu:626-634):
     # built, parity-tested and measured, not dispatched (BN=128)
     explicit |= {c.name for c in cfgs if c.block_n == 128}
+    # the quad grouping without a mask: parity-tested, slower than the
+    # persistent tier wherever it could run (profiles/r05_w4q_ab.jsonl)
+    explicit |= {c.name for c in cfgs if "_asm_quad_noncausal" in c.name}
     # head_dim 64 of the asm W4 tier runs the ping-pong persistent twins
     w4 = {n for n in used if "_asm_persistent_" in n}
     assert w4, "the W4 tier is dispatched"
@@ -306,7 +310,7 @@ def test_split_plan_and_workspace_entry():
     fa = _fa()
     lib = fa.load_library()
     # the dispatcher splits long causal launches short of the persistent tier
-    for b, h, s in ((1, 12, 4096), (1, 4, 8192), (1, 2, 16384), (1, 1, 32768)):
+    for b, h, s in ((1, 6, 8192), (1, 4, 8192), (1, 2, 16384), (1, 1, 32768)):
         t = lib.fa_fwd_split_pieces(b, h, s, 128, 1)
         assert t >= 4, (b, h, s)
         need = lib.fa_fwd_ws_bytes(b, h, s, 128, 1, 0)

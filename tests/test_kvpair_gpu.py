@@ -94,16 +94,16 @@ def test_kvpair_causal_row0_is_v0(kind):
 def test_kvpair_is_a_short_tier():
     fa = _fa()
     cfgs = fa.configs()
-    # more than a round of paired blocks (non-causal), causal launches past
-    # S=2048 short of the KV-quad's and the persistent tier's shapes
+    # between the KV-quad's and the paired tier's non-causal shapes, causal
+    # launches past S=4096 short of the KV-quad's and the persistent tier's
     assert "_kvpair_" in cfgs[fa.select_config(1, 20, 1024, False)].name
-    assert "_kvpair_" in cfgs[fa.select_config(1, 12, 4096, True)].name
+    assert "_kvpair_" in cfgs[fa.select_config(1, 6, 8192, True)].name
     # dispatched at such a shape: same result as the forced config
     g = torch.Generator(device="cuda")
     g.manual_seed(4)
-    q, k, v = (torch.empty(1, 12, 4096, 128, dtype=torch.float16, device="cuda")
+    q, k, v = (torch.empty(1, 6, 8192, 128, dtype=torch.float16, device="cuda")
                .uniform_(-0.5, 0.5, generator=g) for _ in range(3))
-    a = fa.flash_attention_fwd(q, k, v, causal=True, config=fa.select_config(1, 12, 4096, True))
+    a = fa.flash_attention_fwd(q, k, v, causal=True, config=fa.select_config(1, 6, 8192, True))
     b = fa.flash_attention_fwd(q, k, v, causal=True, config=_kvpair(True))
     torch.cuda.synchronize()
     assert torch.equal(a, b)

@@ -55,7 +55,7 @@ def _torch_ref(q, k, v):
 # launches short of the persistent tier); > 0 forces that piece length, so
 # short and ragged shapes, 2..8 pieces per block and pieces shorter than the
 # diagonal's 4 tiles are covered too
-SHAPES = [(1, 12, 4096, 0), (1, 8, 4096, 22), (2, 3, 5000, 0), (1, 4, 8192, 0), (1, 32, 512, 4), (1, 32, 768, 4),
+SHAPES = [(1, 12, 4096, 44), (1, 8, 4096, 22), (2, 3, 5000, 0), (1, 4, 8192, 0), (1, 32, 512, 4), (1, 32, 768, 4),
           (1, 32, 1024, 6), (2, 8, 1000, 5), (1, 16, 2048, 12), (3, 5, 1500, 4), (1, 1, 512, 4),
           (1, 2, 2048, 4), (2, 2, 700, 2), (1, 3, 512, 1)]
 
@@ -95,7 +95,7 @@ def test_split_peaked(shape):
     assert err <= TOL, err
 
 
-@pytest.mark.parametrize("shape", [(1, 32, 1024, 6), (2, 8, 1000, 4), (1, 12, 4096, 0)],
+@pytest.mark.parametrize("shape", [(1, 32, 1024, 6), (2, 8, 1000, 4), (1, 12, 4096, 44)],
                          ids=lambda s: "x".join(map(str, s)))
 def test_split_bf16(shape):
     fa = _fa()

@@ -1,9 +1,10 @@
-"""Paired short-sequence tier (bm128_bn64_w4x32_m16_asm_pair_*, fa_w4p_kernel.hpp +
-the generated item program fa_w4p_item.inc).
+"""Multi-block short-sequence tier (bm128_bn64_w4x32_m16_asm_pair_*: two 64-row
+query blocks per workgroup, bm256_bn64_w4x64_m16_asm_quad_*: four;
+fa_w4p_kernel.hpp + the generated item program fa_w4p_item.inc).
 
-A workgroup holds two 64-row query blocks of one head (causal: the heavy
-block nqb-1-r with the light block r) on one shared K/V stream, 16 rows of
-each per wave.  Its rescale decision is per 16-row block (the 8-wave kernels
+A workgroup holds two or four 64-row query blocks of one head (causal: pairs
+of the heavy block nqb-1-r with the light block r) on one shared K/V stream,
+16 rows of each per wave.  Its rescale decision is per 16-row block (the 8-wave kernels
 take it per 32-row wave), so outputs are compared with the oracle (the
 reference's cpu_attention restatement) on sampled heads and with an fp32
 torch attention on every head, both at the 1e-3 gate; bf16 against the fp32
@@ -21,6 +22,7 @@ import oracle  # noqa: E402  (test infrastructure)
 pytestmark = pytest.mark.gpu
 TOL = 1e-3
 PAIR = "bm128_bn64_w4x32_m16_asm_pair"
+QUAD = "bm256_bn64_w4x64_m16_asm_quad"
 
 
 def _fa():
@@ -61,9 +63,9 @@ def _torch_ref(q, k, v, causal):
     return out
 
 
-def _check(b, h, s, causal, seed, scale=1.0, dtype=torch.float16, oracle_heads=True):
+def _check(b, h, s, causal, seed, scale=1.0, dtype=torch.float16, oracle_heads=True, tier=PAIR):
     fa = _fa()
-    pre = PAIR if dtype == torch.float16 else "bf16_" + PAIR
+    pre = tier if dtype == torch.float16 else "bf16_" + tier
     q, k, v = (_rand((b, h, s, 128), seed + i, scale if i < 2 else 1.0, dtype) for i in range(3))
     out = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(pre)[causal])
     torch.cuda.synchronize()
@@ -96,17 +98,22 @@ SHAPES = [
 ]
 
 
+TIERS = [PAIR, QUAD]
+
+
+@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
-def test_pair_matches_oracle(shape, causal):
-    _check(*shape, causal, seed=700)
+def test_pair_matches_oracle(shape, causal, tier):
+    _check(*shape, causal, seed=700, tier=tier)
 
 
+@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("s", [256, 1000, 2048])
-def test_pair_peaked_rescale(s, causal):
+def test_pair_peaked_rescale(s, causal, tier):
     # Q, K x4: row maxima keep growing past the 2^8 threshold -> the slow paths
-    _check(1, 8, s, causal, seed=710, scale=4.0)
+    _check(1, 8, s, causal, seed=710, scale=4.0, tier=tier)
 
 
 def _random_shapes(n, seed):
@@ -115,16 +122,18 @@ def _random_shapes(n, seed):
             for _ in range(n)]
 
 
+@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("shape", _random_shapes(6, 2027), ids=lambda s: "x".join(map(str, s)))
-def test_pair_random_shapes(shape, causal):
-    _check(*shape, causal, seed=720)
+def test_pair_random_shapes(shape, causal, tier):
+    _check(*shape, causal, seed=720, tier=tier)
 
 
+@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("shape", [(1, 32, 1024), (1, 8, 1000), (2, 3, 320)], ids=lambda s: "x".join(map(str, s)))
-def test_pair_bf16(shape, causal):
-    _check(*shape, causal, seed=730, dtype=torch.bfloat16)
+def test_pair_bf16(shape, causal, tier):
+    _check(*shape, causal, seed=730, dtype=torch.bfloat16, tier=tier)
 
 
 def _sample_rows(s, n=12):
@@ -170,9 +179,24 @@ def test_pair_causal_row0_and_ones():
         assert torch.equal(o1, ones)
 
 
-def test_pair_deterministic():
+@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
+def test_pair_deterministic(tier):
     fa = _fa()
     q, k, v = (_rand((1, 32, 1024, 128), 750 + i) for i in range(3))
-    a = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(PAIR)[True])
-    b = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(PAIR)[True])
+    a = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(tier)[True])
+    b = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(tier)[True])
     assert torch.equal(a, b)
+
+
+def test_quad_matches_pair_causal_row0_and_ones():
+    """the quad grouping: causal row 0 = V[0], V = 1 -> O = 1, and within the
+    1e-3 gate of the pair grouping (same arithmetic per block)"""
+    fa = _fa()
+    q, k, v = (_rand((1, 8, 2048, 128), 770 + i) for i in range(3))
+    a = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(QUAD)[True])
+    b = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(PAIR)[True])
+    assert torch.equal(a[:, :, 0], v[:, :, 0])
+    assert (a.float() - b.float()).abs().max().item() <= TOL
+    ones = torch.ones_like(v)
+    o1 = fa.flash_attention_fwd(q, k, ones, causal=True, config=_ids(QUAD)[True])
+    assert torch.equal(o1, ones)
