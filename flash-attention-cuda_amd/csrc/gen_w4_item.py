@@ -1235,7 +1235,10 @@ def read_item(st, causal):
     rsrc(st, 76, ST0, ST1, "s57")                          # RO
     st.raw(f"v_readfirstlane_b32 {ST0}, v142")
     st.raw(f"v_readfirstlane_b32 {ST1}, v143")
-    st.raw("s_lshr_b32 s57, s57, 6")                      # LSE bytes = O bytes / 64
+    # LSE bytes = O bytes * 4 / ROWB (one fp32 per row of ROWB() O bytes)
+    shift = (ROWB() // 4).bit_length() - 1
+    assert 4 << shift == ROWB()
+    st.raw(f"s_lshr_b32 s57, s57, {shift}")
     rsrc(st, 80, ST0, ST1, "s57")                          # RL
     st.raw(f"v_readfirstlane_b32 {QW}, v137")             # q0
     st.raw(f"s_add_u32 {QW}, {QW}, %[woff]")              # + 64 wave
@@ -1336,6 +1339,33 @@ def zero_state(st):
         st.raw(f"v_mov_b32 {MREF[b]}, 0")
 
 
+# fp16 Q * c and O / l rounded ONCE, by mixed-precision fmas into the two
+# halves of the packed result (v_fma_mixlo/hi_f16: fma(a, s, -0), the exact
+# product rounded straight to fp16, signed zeros kept) -- one VALU per two
+# elements fewer than the fp32 product + v_cvt_pk, whose two roundings
+# M16::scale_q / store_o use.  Experiment (W4_XP=mix), off: 128 fewer VALU
+# per item measured neutral on every shape (headline 1210.8 vs 1213.1,
+# S=8192 causal 1365.0 vs 1368.7, short causal W4P -0.6 to -1.3 %;
+# profiles/r05_ab_mix.jsonl, 290 W4/W4P/split GPU tests green with it).
+# bf16 has no mix form.
+MIX_XP = "mix" in XP
+
+
+def mix():
+    return MIX_XP and not DT["bf16"]
+
+
+def mix_pk(dst, a, b, s, f16src=False):
+    """dst = fp16(a s) | fp16(b s) << 16 (f32 a, b; f16src: a = b = the
+    packed fp16 pair, low then high half)"""
+    if f16src:
+        return [valu(f"v_fma_mixlo_f16 {dst}, {a}, {s}, neg(0) op_sel_hi:[1,0,0]", r=[a], w=[dst]),
+                valu(f"v_fma_mixhi_f16 {dst}, {b}, {s}, neg(0) op_sel:[1,0,0] op_sel_hi:[1,0,0]",
+                     r=[b, dst], w=[dst])]
+    return [valu(f"v_fma_mixlo_f16 {dst}, {a}, {s}, neg(0)", r=[a, s], w=[dst]),
+            valu(f"v_fma_mixhi_f16 {dst}, {b}, {s}, neg(0)", r=[b, s, dst], w=[dst])]
+
+
 def q_scale(st):
     """Q * c (fp32 product, rounded to fp16 once: M16::scale_q) from v0-63
     into AGPRs, eight elements at a time in the (free) V^T fragment registers"""
@@ -1344,6 +1374,13 @@ def q_scale(st):
         lo = {x: f"v{144 + 3 * (x - x0)}" for x in xs}
         hi = {x: f"v{145 + 3 * (x - x0)}" for x in xs}
         pk = {x: f"v{146 + 3 * (x - x0)}" for x in xs}
+        if mix():
+            for x in xs:
+                for op in mix_pk(pk[x], f"v{x}", f"v{x}", "%[c]", f16src=True):
+                    st.raw(op.text)
+            for x in xs:
+                st.raw(f"v_accvgpr_write_b32 a{144 + x}, {pk[x]}")
+            continue
         if DT["bf16"]:
             for x in xs:  # bf16 -> fp32 is exact: the 16 bits move to the top half
                 st.raw(f"v_lshlrev_b32_e32 {lo[x]}, 16, v{x}")
@@ -1556,16 +1593,21 @@ def epilogue_ops(split, ro=RO, rowbase=ST1, zero_o=False):
                     E(valu(f"v_accvgpr_read_b32 {d[4 * x + i]}, {src}", r=[src], w=[d[4 * x + i]]))
                     if zero_o and not mfz():
                         E(valu(f"v_accvgpr_write_b32 {O(b, e, i)}, 0", w=[O(b, e, i)]))
-                if DIAG in ("raw", "l"):
+                if DIAG in ("raw", "l") or mix():
                     continue
                 for i in range(4):
                     E(valu(f"v_mul_f32_e32 {d[4 * x + i]}, {d[4 * x + i]}, {inv}", r=[d[4 * x + i], inv], w=[d[4 * x + i]]))
             # X = e even pair -> v152,153 ; Y = e odd -> v154,155
             X, Y = ["v152", "v153"], ["v154", "v155"]
-            E(valu(f"{DT['cvt_pk']} {X[0]}, {d[0]}, {d[1]}", r=d[0:2], w=[X[0]]))
-            E(valu(f"{DT['cvt_pk']} {X[1]}, {d[2]}, {d[3]}", r=d[2:4], w=[X[1]]))
-            E(valu(f"{DT['cvt_pk']} {Y[0]}, {d[4]}, {d[5]}", r=d[4:6], w=[Y[0]]))
-            E(valu(f"{DT['cvt_pk']} {Y[1]}, {d[6]}, {d[7]}", r=d[6:8], w=[Y[1]]))
+            if mix() and DIAG not in ("raw", "l"):
+                for k, dst in enumerate(X + Y):
+                    for op in mix_pk(dst, d[2 * k], d[2 * k + 1], inv):
+                        E(op)
+            else:
+                E(valu(f"{DT['cvt_pk']} {X[0]}, {d[0]}, {d[1]}", r=d[0:2], w=[X[0]]))
+                E(valu(f"{DT['cvt_pk']} {X[1]}, {d[2]}, {d[3]}", r=d[2:4], w=[X[1]]))
+                E(valu(f"{DT['cvt_pk']} {Y[0]}, {d[4]}, {d[5]}", r=d[4:6], w=[Y[0]]))
+                E(valu(f"{DT['cvt_pk']} {Y[1]}, {d[6]}, {d[7]}", r=d[6:8], w=[Y[1]]))
             for dw in range(2):
                 E(valu(f"v_permlane16_swap_b32 {X[dw]}, {Y[dw]}", r=[X[dw], Y[dw]], w=[X[dw], Y[dw]]))
             pol = OPOL if not split else " sc1"

@@ -571,6 +571,13 @@ def q_scale(st):
         lo = {x: f"v{144 + 3 * (x - x0)}" for x in xs}
         hi = {x: f"v{145 + 3 * (x - x0)}" for x in xs}
         pk = {x: f"v{146 + 3 * (x - x0)}" for x in xs}
+        if w4.mix():  # one rounding: gen_w4_item.mix_pk
+            for x in xs:
+                for op in w4.mix_pk(pk[x], f"v{x}", f"v{x}", "%[c]", f16src=True):
+                    st.raw(op.text)
+            for x in xs:
+                st.raw(f"v_accvgpr_write_b32 a{144 + x}, {pk[x]}")
+            continue
         if DT["bf16"]:
             for x in xs:
                 st.raw(f"v_lshlrev_b32_e32 {lo[x]}, 16, v{x}")
@@ -729,14 +736,19 @@ def epilogue_block(st, b):
             for i in range(4):
                 d = EPI[4 * x + i]
                 st.emit(valu(f"v_accvgpr_read_b32 {d}, {O(b, e, i)}", r=[O(b, e, i)], w=[d]))
-            for i in range(4):
+            for i in range(4 if not w4.mix() else 0):
                 d = EPI[4 * x + i]
                 st.emit(valu(f"v_mul_f32_e32 {d}, {d}, {inv}", r=[d, inv], w=[d]))
         X, Y = XY[0:2], XY[2:4]
-        st.emit(valu(f"{DT['cvt_pk']} {X[0]}, {EPI[0]}, {EPI[1]}", r=EPI[0:2], w=[X[0]]))
-        st.emit(valu(f"{DT['cvt_pk']} {X[1]}, {EPI[2]}, {EPI[3]}", r=EPI[2:4], w=[X[1]]))
-        st.emit(valu(f"{DT['cvt_pk']} {Y[0]}, {EPI[4]}, {EPI[5]}", r=EPI[4:6], w=[Y[0]]))
-        st.emit(valu(f"{DT['cvt_pk']} {Y[1]}, {EPI[6]}, {EPI[7]}", r=EPI[6:8], w=[Y[1]]))
+        if w4.mix():
+            for k, dst in enumerate(X + Y):
+                for op in w4.mix_pk(dst, EPI[2 * k], EPI[2 * k + 1], inv):
+                    st.emit(op)
+        else:
+            st.emit(valu(f"{DT['cvt_pk']} {X[0]}, {EPI[0]}, {EPI[1]}", r=EPI[0:2], w=[X[0]]))
+            st.emit(valu(f"{DT['cvt_pk']} {X[1]}, {EPI[2]}, {EPI[3]}", r=EPI[2:4], w=[X[1]]))
+            st.emit(valu(f"{DT['cvt_pk']} {Y[0]}, {EPI[4]}, {EPI[5]}", r=EPI[4:6], w=[Y[0]]))
+            st.emit(valu(f"{DT['cvt_pk']} {Y[1]}, {EPI[6]}, {EPI[7]}", r=EPI[6:8], w=[Y[1]]))
         for dw in range(2):
             st.emit(valu(f"v_permlane16_swap_b32 {X[dw]}, {Y[dw]}", r=[X[dw], Y[dw]], w=[X[dw], Y[dw]]))
         st.emit(vmem(f"buffer_store_dwordx4 v[152:155], {T[7]}, {RO}, 0 offen offset:{64 * ep} sc1",

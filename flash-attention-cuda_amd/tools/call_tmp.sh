@@ -1,9 +1,14 @@
-#!/bin/bash
-# final-tree pass: gpu_check (tests, smoke, bench, rocprof kernel trace, harness), then the per-tier table
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-ROUND=r04 bash flash-attention-cuda_amd/tools/gpu_check.sh || exit 1
-bash flash-attention-cuda_amd/tools/tier_pmc.sh > gpurun_out/tier_pmc_summary.txt 2>&1
-rc=$?
-grep -v amdgpu.ids gpurun_out/tier_pmc_summary.txt
-exit $rc
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests/test_w4_gpu.py tests/test_w4p_gpu.py tests/test_split_gpu.py tests/test_persistent_gpu.py tests/test_fullsize_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r05_pytest_mix.log 2>&1 || { tail -30 gpurun_out/r05_pytest_mix.log; exit 1; }
+tail -2 gpurun_out/r05_pytest_mix.log
+AB="timeout -k 10 300 python flash-attention-cuda_amd/tools/ab.py --configs auto --libs ,nomix"
+O=gpurun_out/r05_ab_mix.jsonl
+$AB --seq 4096 --batch 64 --causal --rounds 9 --iters 10 > $O &&
+$AB --seq 8192 --causal --rounds 9 --iters 20 >> $O &&
+$AB --seq 8192 --rounds 9 --iters 20 >> $O &&
+$AB --seq 1024 --causal --rounds 9 --iters 40 >> $O &&
+$AB --seq 2048 --causal --rounds 9 --iters 40 >> $O &&
+$AB --seq 4096 --batch 64 --causal --rounds 7 --iters 10 --dtype bf16 >> $O || exit 1
+cat $O
