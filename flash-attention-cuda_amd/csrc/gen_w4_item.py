@@ -123,8 +123,8 @@ def NPASS():  # 4-KiB register-staging passes per tile and tensor (256 lanes x 1
     return HDC["hd"] // 32
 
 
-def PASSL():  # LDS stride of a staging pass (its rows in 256-B slots)
-    return 256 * (4096 // ROWB())
+def PASSL():  # LDS stride of a 4-KiB staging pass (the images are packed: 4 KiB)
+    return 4096
 # causal diagonal tile masked block by block inside phase A (W4_DIAG_FAST=0:
 # the general mask after phase A, for A/B)
 DIAG_FAST = os.environ.get("W4_DIAG_FAST", "1") == "1"
@@ -450,15 +450,18 @@ def kslot(cb, t):
     return 4 * (cb & 1) + t if NT() == 4 else 2 * cb + t
 
 
+# K / V images hold packed rows (fa_w4_kernel.hpp: 256-B rows at head_dim
+# 128, 128-B rows at 64): a 16-key block is 16 ROWB() bytes of K, a 32-key
+# step 32 ROWB() of V
 def k_read(t, cb, slot, kb):
-    return dsr(f"ds_read_b128 {KF(slot)}, {KADDR[t]} offset:{kb + 4096 * cb}", KF(slot), KADDR[t])
+    return dsr(f"ds_read_b128 {KF(slot)}, {KADDR[t]} offset:{kb + 16 * ROWB() * cb}", KF(slot), KADDR[t])
 
 
 def v_reads(u, e, slot, vb):
-    off = vb + 8192 * u + 512 * (e >> 1)
+    off = vb + 32 * ROWB() * u + 512 * (e >> 1)
     a = VADDR[e & 1]
     return [dsr(f"ds_read_b64_tr_b16 {VF(slot, 0)}, {a} offset:{off}", VF(slot, 0), a),
-            dsr(f"ds_read_b64_tr_b16 {VF(slot, 1)}, {a} offset:{off + 4096}", VF(slot, 1), a)]
+            dsr(f"ds_read_b64_tr_b16 {VF(slot, 1)}, {a} offset:{off + 16 * ROWB()}", VF(slot, 1), a)]
 
 
 def qk_chain(b, cb, slots):
@@ -553,10 +556,14 @@ PEND = "s71"         # 1: the last phase B's row sums are pending (RSA)
 
 
 def dma():
-    """LDS-DMA staging (head_dim 128); head_dim 64 stages through registers:
-    its rows fill half of an image's 256-B slots, so a lane-linear DMA piece
-    would move half padding"""
-    return DMA_ON and HDC["hd"] == 128
+    """LDS-DMA staging (both head dims: the images are packed, so a
+    lane-linear 1-KiB piece carries no padding -- four pieces per wave and
+    tensor at head_dim 128, two at 64)"""
+    return DMA_ON
+
+
+def npiece():  # LDS-DMA pieces per wave, tile and tensor (1 KiB each)
+    return TILEB() // 4096
 
 
 def sg0():  # prologue stage-0 loads in flight (none under DMA)
@@ -602,29 +609,36 @@ def dma_loads(p):
     piece (one MFMA between the M0 write and the load: its wait state); then
     the descriptors advance one tile"""
     out = []
-    for i in range(4):
+    for i in range(npiece()):
         out.append(salu(f"s_add_u32 m0, %[dmab], {KBUF[p] + 1024 * i}"))
         out.append(vmem(f"buffer_load_dwordx4 {KD(i)}, {SK}, 0 offen lds", r=[KD(i)]))
-    for i in range(4):
+    for i in range(npiece()):
         out.append(salu(f"s_add_u32 m0, %[dmab], {VBUF[1 - p] + 1024 * i}"))
         out.append(vmem(f"buffer_load_dwordx4 {VD(i)}, {SV}, 0 offen lds", r=[VD(i)]))
-    out += [salu("s_add_u32 s40, s40, 0x4000"), salu("s_addc_u32 s41, s41, 0"),
-            salu(f"s_sub_i32 {SKREM}, {SKREM}, 0x4000"), salu(f"s_max_i32 s42, {SKREM}, 0"),
-            salu("s_add_u32 s44, s44, 0x4000"), salu("s_addc_u32 s45, s45, 0"),
-            salu(f"s_sub_i32 {SVREM}, {SVREM}, 0x4000"), salu(f"s_max_i32 s46, {SVREM}, 0")]
+    tb = hex(TILEB())
+    out += [salu(f"s_add_u32 s40, s40, {tb}"), salu("s_addc_u32 s41, s41, 0"),
+            salu(f"s_sub_i32 {SKREM}, {SKREM}, {tb}"), salu(f"s_max_i32 s42, {SKREM}, 0"),
+            salu(f"s_add_u32 s44, s44, {tb}"), salu("s_addc_u32 s45, s45, 0"),
+            salu(f"s_sub_i32 {SVREM}, {SVREM}, {tb}"), salu(f"s_max_i32 s46, {SVREM}, 0")]
     return out
 
 
 def dma_setup(st):
     """M0 saved; per-pass DMA source offsets from the lane constants
-    (kdma = piece 0's, K(i) = (kdma + 1024 i) ^ 64 i; vdma = piece 0's, V(i) =
-    vdma + 2048 (i >> 1) + 128 (i & 1), chunk bit 1 flipped for i >= 2)"""
+    (kdma = piece 0's, K(i) = (kdma + 1024 i) ^ 64 i; vdma = piece 0's; head
+    dim 128: V(i) = vdma + 2048 (i >> 1) + 128 (i & 1), chunk bit 1 flipped
+    for i >= 2; head dim 64: V(1) = (vdma + 1024) ^ 32 -- 8 rows on, whose
+    chunk XOR (row >> 2) & 3 differs by 2)"""
     st.raw(f"s_mov_b32 {SM0}, m0")
     st.raw(f"v_mov_b32 {KD(0)}, %[kdma]")
     st.raw(f"v_mov_b32 {VD(0)}, %[vdma]")
-    for i in range(1, 4):
+    for i in range(1, npiece()):
         st.raw(f"v_add_u32 {KD(i)}, {1024 * i}, %[kdma]")
         st.raw(f"v_xor_b32 {KD(i)}, {64 * i}, {KD(i)}")
+        if HDC["hd"] == 64:
+            st.raw(f"v_add_u32 {VD(i)}, 1024, %[vdma]")
+            st.raw(f"v_xor_b32 {VD(i)}, 32, {VD(i)}")
+            continue
         st.raw(f"v_add_u32 {VD(i)}, {2048 * (i >> 1) + 128 * (i & 1)}, %[vdma]")
         if i >= 2:
             st.raw(f"v_xor_b32 {VD(i)}, 32, {VD(i)}")
