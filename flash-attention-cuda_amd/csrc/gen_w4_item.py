@@ -524,7 +524,13 @@ STAGE2 = "stage1" not in XP
 LD_AT = int(os.environ.get("W4_LD_AT", "18"))
 LD_SP = int(os.environ.get("W4_LD_SP", "2"))
 DMA_AT = int(os.environ.get("W4_DMA_AT", "2"))  # first phase-A gap of the DMA sequence
-DMA_SP = int(os.environ.get("W4_DMA_SP", "1"))  # gaps between its instructions
+# gaps between its instructions: 1 at head_dim 128, 2 at 64 (+0.1-1.6 % over
+# 1 there, profiles/r05_ab_d64var.jsonl "dsp2")
+DMA_SP_ENV = os.environ.get("W4_DMA_SP")
+
+
+def dma_sp():
+    return int(DMA_SP_ENV) if DMA_SP_ENV else (1 if HDC["hd"] == 128 else 2)
 CVT0 = "cvt0" in XP
 CVT_EARLY = "cvtearly" in XP
 # the 8 row-sum MFMAs of PV(j) at the start of phase A(j+1), under the K
@@ -535,6 +541,11 @@ RSA = "rsa" in XP
 # -0.5 %, profiles/r04_ab_w4_one_barrier_seam{,_d64}.jsonl; W4_XP=twobar
 # keeps two at 128 too)
 ONEBAR_XP = "twobar" not in XP
+ONEBAR64_XP = "onebar64" in XP
+
+
+def onebar():
+    return ONEBAR_XP and (HDC["hd"] == 128 or ONEBAR64_XP)
 # gap of a chain's maxima within chain x + LAG, and the first phase-B gap of
 # phase A's leftover maxima: one gap later than the hazard windows need
 # spares 3 of a tile's 5 s_nop (profiles/r04_ab_w4_nop_trim*.jsonl)
@@ -770,7 +781,7 @@ def phase_a(st, p, with_max, diag=False):
     # stage traffic: LDS writes in cb 0, loads in cb 1
     if "nostage" not in XP and dma():
         for i, ld in enumerate(stage_loads(p=p)):
-            put((4 + i) if diag else (DMA_AT + DMA_SP * i), ld)
+            put((4 + i) if diag else (DMA_AT + dma_sp() * i), ld)
     elif "nostage" not in XP and STAGE2:
         for i, ld in enumerate(stage_loads(1 - p)):
             if HDC["hd"] == 128:
@@ -1483,7 +1494,7 @@ def prologue(st, causal, split=False):
     for i in range(NPASS()):
         st.raw(f"ds_write_b128 %[klds], {R('v', 112 + 4 * i, 4)} offset:{KBUF[0] + PASSL() * i}")
     q_scale(st)
-    if ONEBAR_XP and HDC["hd"] == 128:
+    if onebar():
         # V(0), K(1) (prefetched after Q, K(0)) landed under the Q scaling:
         # into their LDS images before the same barrier as K(0) -- the
         # previous item's last barrier freed every image
@@ -1521,7 +1532,7 @@ def prologue(st, causal, split=False):
     prostamp(st, 3)  # -> first softmax + exp2 done
     # V(0), K(1) landed: into their LDS images (warm with the deferred
     # epilogue: its 16 O stores are the youngest, behind stage 0's 8 loads)
-    if ONEBAR_XP and HDC["hd"] == 128:
+    if onebar():
         pass
     elif xovl:
         cw, cd = newlabel("coldw"), newlabel("waitdone")
@@ -1534,7 +1545,7 @@ def prologue(st, causal, split=False):
         st.label(cd)
     else:
         st.raw(f"s_waitcnt vmcnt({sg0()})")
-    if not (ONEBAR_XP and HDC["hd"] == 128):
+    if not (onebar()):
         for i in range(NPASS()):
             st.raw(f"ds_write_b128 %[vlds], {vst(i, 1)} offset:{VBUF[0] + PASSL() * i}")
             st.raw(f"ds_write_b128 %[klds], {kst(i, 1)} offset:{KBUF[1] + PASSL() * i}")

@@ -41,10 +41,16 @@ for rep in range(a.reps + 1):
     t0 = min(st)
     ends = sorted((e - t0) / 100.0 for e in en)  # us
     starts = sorted((s - t0) / 100.0 for s in st)
+    xcc = [(buf[4 * i + 2] >> 32) & 0xff for i in range(n)]
+    by_x = {}
+    for i in range(n):
+        by_x.setdefault(xcc[i], []).append((en[i] - t0) / 100.0)
     span = ends[-1]
     mean_end = sum(ends) / n
     res.append({"span_us": round(span, 1), "mean_end_us": round(mean_end, 1),
                 "p10_end_us": round(ends[n // 10], 1), "min_end_us": round(ends[0], 1),
                 "idle_tail_frac": round((span - mean_end) / span, 4),
-                "start_skew_us": round(starts[-1], 2)})
+                "start_skew_us": round(starts[-1], 2),
+                # per XCD: mean / max workgroup end (is the spread per die or per CU?)
+                "xcd_end_us": {x: [round(sum(v) / len(v), 1), round(max(v), 1)] for x, v in sorted(by_x.items())}})
 print(json.dumps({"seq": a.seq, "batch": a.batch, "heads": a.heads, "causal": a.causal, "reps": res}))
