@@ -23,7 +23,7 @@ Derived per launch (first launch of each shape dropped):
                 this is below the un-profiled HIP-event TFLOP/s)
   ghz_in_kernel = s_memtime cycles / s_memrealtime time per workgroup, median,
                 from the stamps build after >= 2 s of launches (tier_pmc.py
-                clocks), W4 rows only (the other tiers' stamps builds stamp
+                clocks), W4 and W4P rows only (the other tiers' stamps builds stamp
                 every loop phase); eff_clock is left out below 0.3 ms, where it
                 reads high, and above 2.4 GHz
   frac_nominal = TFLOP/s (un-profiled, HIP events) / 2516.6
@@ -37,6 +37,7 @@ import sys
 
 SHAPES = [  # (label, batch, heads, seq, causal[, forced tier name | "auto"])
     ("cfg0_s512_noncausal", 1, 32, 512, False),
+    ("s512_causal", 1, 32, 512, True),
     ("cfg1_s1024_causal", 1, 32, 1024, True),
     ("s1024_noncausal", 1, 32, 1024, False),
     ("s2048_causal", 1, 32, 2048, True),
@@ -60,6 +61,9 @@ SHAPES = [  # (label, batch, heads, seq, causal[, forced tier name | "auto"])
     ("bn128_s8192_noncausal", 1, 32, 8192, False, "bm128_bn128_w4_m16_noncausal"),
     ("bn128_s8192_causal", 1, 32, 8192, True, "bm128_bn128_w4_m16_causal"),
     ("pingpong_item_s8192_causal", 1, 32, 8192, True, "bm256_bn64_w8_m16_pingpong_causal"),
+    # the KV-pair the round-5 paired / quad tier replaced on short causal launches
+    ("kvpair_cfg1_s1024_causal", 1, 32, 1024, True, "bm128_bn64_w8_m16_kvpair_causal"),
+    ("kvpair_s2048_causal", 1, 32, 2048, True, "bm128_bn64_w8_m16_kvpair_causal"),
     # head_dim 64 (label prefix d64_: the dispatcher's d64 twin, W4 on these)
     ("d64_target_s8192_causal", 1, 32, 8192, True, "auto"),
     ("d64_headline_b64_s4096_causal", 64, 32, 4096, True, "auto"),
@@ -238,7 +242,8 @@ def summary(timing_jsonl, mfma_dir, fetch_dir, write_dir, out, clocks_jsonl=None
             # the loop (W4: one start / end record per workgroup); the other
             # tiers' diagnostic builds stamp every phase, which moves their clock
             "ghz_in_kernel": (clk.get(label, {}).get("ghz_in_kernel_median")
-                              if "asm_persistent" in t["config"] else None),
+                              if any(x in t["config"] for x in ("asm_persistent", "asm_pair", "asm_quad"))
+                              else None),
             "ms_profiled": round(mean(dur) / 1e6, 4), "tflops_profiled": round(tf_prof, 1),
 
             "hbm_bytes": int(hbm), "alg_bytes": int(t["alg_bytes"]),
