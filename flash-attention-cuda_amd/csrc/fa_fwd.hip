@@ -519,13 +519,29 @@ static int check_args(const void* q, const void* k, const void* v, const void* o
   return FA_OK;
 }
 
+// W4 launches with a cross-XCD tail pool (fa_w4_kernel.hpp): the snake order
+// (not the causal pairs of <= 64 heads) with >= 16 rounds per XCD list
+static bool w4_pool_on(const Config& cfg, long long bh, int nqb, long long blocks) {
+  if (cfg.kind != 5 || blocks < 8) return false;
+  if (cfg.info.causal && bh <= 64 && bh % 8 == 0 && nqb % 2 == 0) return false;  // pairs
+  const long long per_xcd = (bh * nqb + 7) / 8, c = blocks / 8;
+  return w4_pool_rounds((int)std::min<long long>((per_xcd + c - 1) / c, 1 << 30)) > 0;
+}
+
+static long long persistent_blocks(const Config& cfg, long long bh, int nqb) {
+  // one workgroup per CU, 8 per XCD group; never more than the items per XCD
+  const long long per_xcd = (bh & 7) == 0 ? (bh / 8) * nqb : (bh * nqb + 7) / 8;
+  const long long c = std::min<long long>(std::max(1, num_cus() / 8), per_xcd);
+  return 8 * c;
+}
+
 static int launch(int id, const void* q, const void* k, const void* v, void* o, int bh,
                   int seq_len, int num_splits, float* part_o, float* part_ml,
-                  hipStream_t stream) {
+                  hipStream_t stream, unsigned* pool_ctr = nullptr) {
   const Config& cfg = kConfigs[id];
   int rc = prepare(id);
   if (rc != FA_OK) return rc;
-  FwdParams p;
+  FwdParams p = {};
   p.q = static_cast<const f16*>(q);
   p.k = static_cast<const f16*>(k);
   p.v = static_cast<const f16*>(v);
@@ -543,13 +559,8 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   p.band = bh <= 64 ? 1 : 16;
   long long blocks = (long long)p.nqb * bh * num_splits;
   if (blocks > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
-  if (cfg.kind == 2 || cfg.kind == 5) {
-    // one workgroup per CU, 8 per XCD group; never more than the items per XCD
-    const long long per_xcd = (bh & 7) == 0 ? (long long)(bh / 8) * p.nqb
-                                            : ((long long)bh * p.nqb + 7) / 8;
-    const long long c = std::min<long long>(std::max(1, num_cus() / 8), per_xcd);
-    blocks = 8 * c;
-  }
+  if (cfg.kind == 2 || cfg.kind == 5) blocks = persistent_blocks(cfg, bh, p.nqb);
+  if (pool_ctr && w4_pool_on(cfg, bh, p.nqb, blocks)) p.ws_ctr = pool_ctr;
 
   hipLaunchKernelGGL(cfg.fn, dim3((unsigned)blocks), dim3(cfg.info.waves * 64),
                      cfg.info.lds_bytes, stream, p);
@@ -604,7 +615,7 @@ static int launch_config(int config_id, int dtype, const void* q, const void* k,
 // dispatcher tier, as the twin for this dtype / head_dim
 static int launch_auto(int dtype, const void* q, const void* k, const void* v, void* o,
                        int batch, int heads, int seq_len, int head_dim, int causal,
-                       void* hip_stream);
+                       void* hip_stream, unsigned* pool_ctr = nullptr);
 
 }  // namespace fa
 
@@ -701,18 +712,29 @@ static int select_tier(int batch, int heads, int seq_len, int causal, bool pair)
 namespace fa {
 static int launch_auto(int dtype, const void* q, const void* k, const void* v, void* o,
                            int batch, int heads, int seq_len, int head_dim, int causal,
-                           void* hip_stream) {
+                           void* hip_stream, unsigned* pool_ctr) {
   int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
   if (rc != FA_OK) return rc;
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
   const int sel = select_tier(batch, heads, seq_len, causal, head_dim == HD);
   // (head_dim 64 of the W4 tier is the same item program with 2-step QK^T
-  // chains and register-staged K/V: +4-9 % over the 8-wave ping-pong at
-  // head_dim 64, profiles/r04_ab_w4_d64.jsonl)
+  // chains and 8-KiB packed tiles: +4-9 % over the 8-wave ping-pong at
+  // head_dim 64, profiles/r04_ab_w4_d64.jsonl, r05_ab_d64dma.jsonl)
   const int id = twin(sel, dtype, head_dim);
   if (id < 0) return FA_ERR_BAD_CONFIG;
   return launch(id, q, k, v, o, batch * heads, seq_len, 1, nullptr, nullptr,
-                (hipStream_t)hip_stream);
+                (hipStream_t)hip_stream, pool_ctr);
+}
+
+// the default dispatch of a workspace call runs the W4 tier with a cross-XCD
+// tail pool (its counters live in the workspace's counter region)
+static bool auto_pool(int batch, int heads, int seq_len, int head_dim, int causal) {
+  if (batch <= 0 || heads <= 0 || seq_len <= 0 || (head_dim != HD && head_dim != 64)) return false;
+  const int id = twin(select_tier(batch, heads, seq_len, causal, head_dim == HD), FA_DTYPE_F16, head_dim);
+  if (id < 0 || kConfigs[id].kind != 5) return false;
+  const long long bh = (long long)batch * heads;
+  const int nqb = (seq_len + kConfigs[id].info.block_m - 1) / kConfigs[id].info.block_m;
+  return w4_pool_on(kConfigs[id], bh, nqb, persistent_blocks(kConfigs[id], bh, nqb));
 }
 }  // namespace fa
 
@@ -865,8 +887,13 @@ static int launch_ws(int dtype, const void* q, const void* k, const void* v, voi
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
   const SplitPlan sp = split_plan(batch, heads, seq_len, head_dim, causal, piece_tiles);
   if (piece_tiles > 0 && sp.T == 0) return FA_ERR_BAD_CONFIG;  // not a causal d128 split
-  if (sp.T == 0)
-    return launch_auto(dtype, q, k, v, o, batch, heads, seq_len, head_dim, causal, hip_stream);
+  if (sp.T == 0) {
+    // the W4 tier's tail pool when the workspace holds its counters (else
+    // the static order: a workspace is optional there)
+    const bool pool = ws && ws_bytes >= kSplitCtrBytes && auto_pool(batch, heads, seq_len, head_dim, causal);
+    return launch_auto(dtype, q, k, v, o, batch, heads, seq_len, head_dim, causal, hip_stream,
+                       pool ? static_cast<unsigned*>(ws) : nullptr);
+  }
   if (!ws || ws_bytes < sp.bytes()) return FA_ERR_WORKSPACE;
   const int bh = batch * heads;
   return dtype == FA_DTYPE_BF16
@@ -876,7 +903,9 @@ static int launch_ws(int dtype, const void* q, const void* k, const void* v, voi
 
 extern "C" unsigned long long fa_fwd_ws_bytes(int batch, int heads, int seq_len, int head_dim,
                                               int causal, int piece_tiles) {
-  return split_plan(batch, heads, seq_len, head_dim, causal, piece_tiles).bytes();
+  const unsigned long long split = split_plan(batch, heads, seq_len, head_dim, causal, piece_tiles).bytes();
+  if (split || piece_tiles > 0) return split;
+  return auto_pool(batch, heads, seq_len, head_dim, causal) ? kSplitCtrBytes : 0;
 }
 
 extern "C" int fa_fwd_split_pieces(int batch, int heads, int seq_len, int head_dim, int causal) {

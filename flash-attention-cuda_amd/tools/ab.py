@@ -50,13 +50,25 @@ for var in a.libs.split(","):
     libs[var] = fa.load_library()
 # "auto": the default dispatch (flash_attention_fwd with config=None: the
 # workspace split tier where it applies)
-cids = [(var, None if x == "auto" else int(x)) for x in a.configs.split(",") for var in libs]
+# "static": the workspace-free C entry (fa_fwd_f16 / fa_fwd_bf16: the W4 tier's
+# static item order, no tail pool)
+cids = [(var, None if x == "auto" else x if x == "static" else int(x)) for x in a.configs.split(",")
+        for var in libs]
+
+
+def fwd(c):
+    if c[1] != "static":
+        fa.flash_attention_fwd(q, k, v, a.causal, out=o, config=c[1])
+        return
+    fn = fa._lib.fa_fwd_bf16 if dt == torch.bfloat16 else fa._lib.fa_fwd_f16
+    fn(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), a.batch, a.heads, a.seq, a.head_dim,
+       int(a.causal), torch.cuda.current_stream().cuda_stream)
 flops = fa.attention_flops(a.batch, a.heads, a.seq, a.head_dim, a.causal)
 res = {c: [] for c in cids}
 for c in cids:  # warm
     fa._lib = libs[c[0]]
     for _ in range(5):
-        fa.flash_attention_fwd(q, k, v, a.causal, out=o, config=c[1])
+        fwd(c)
 torch.cuda.synchronize()
 for _ in range(a.rounds):
     for c in cids:
@@ -64,11 +76,12 @@ for _ in range(a.rounds):
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st.record()
         for _ in range(a.iters):
-            fa.flash_attention_fwd(q, k, v, a.causal, out=o, config=c[1])
+            fwd(c)
         en.record()
         en.synchronize()
         res[c].append(flops / (st.elapsed_time(en) / a.iters / 1e3) / 1e12)
 names = {c.id: c.name for c in fa.configs()}
+names["static"] = "static (fa_fwd_f16, no workspace)"
 names[None] = "auto(split=%d)" % fa.load_library().fa_fwd_split_pieces(a.batch, a.heads, a.seq, a.head_dim, int(a.causal))
 for c in cids:
     print(json.dumps({"config": names[c[1]], "lib": c[0] or "base", "env": a.env, "seq": a.seq, "head_dim": a.head_dim, "batch": a.batch, "heads": a.heads, "data": a.data, "causal": a.causal,

@@ -123,16 +123,21 @@ unsigned long long fa_splitkv_ml_bytes(int batch, int heads, int seq_len,
  * plus an fp32 log2-sum-exp per row).
  *   piece_tiles = 0: the dispatcher's choice -- fa_fwd_split_pieces() is its
  *     piece length in 64-key tiles, 0 when it does not split this shape (the
- *     _ws entries then run exactly fa_fwd_f16 / fa_fwd_bf16 and ignore the
- *     workspace);
+ *     _ws entries then run the tier fa_fwd_f16 / fa_fwd_bf16 runs; on the
+ *     persistent W4 tier with >= 64 rounds of items per XCD (the B=64
+ *     headline) the workspace's counter region also carries a cross-XCD tail
+ *     pool: the last 1/16 of every XCD's items are claimed at run time, which
+ *     evens out XCDs that run a few % slower -- bit-identical output);
  *   piece_tiles > 0: that piece length (causal, head_dim 128, at most 8
  *     pieces per query block, else FA_ERR_BAD_CONFIG).
- * fa_fwd_ws_bytes() is the workspace the call needs (0: no split).  Its
- * first 64 KB (arrival counters, the same place for every shape) must be
- * zero before the first use; every launch returns the counters it used to
- * zero, so one buffer of the largest size needed serves any sequence of
- * shapes on ONE stream (launches on different streams need their own).  FA_ERR_WORKSPACE if the call splits and workspace is NULL or
- * ws_bytes is short. */
+ * fa_fwd_ws_bytes() is the workspace the call needs (0: neither a split nor
+ * a tail pool; 65536: the tail pool's counters only).  Its first 64 KB
+ * (counters, the same place for every shape) must be zero before the first
+ * use; every launch returns the counters it used to zero, so one buffer of
+ * the largest size needed serves any sequence of shapes on ONE stream
+ * (launches on different streams need their own).  FA_ERR_WORKSPACE if the
+ * call splits and workspace is NULL or ws_bytes is short; a tail-pool shape
+ * with no (or a short) workspace runs the static item order. */
 unsigned long long fa_fwd_ws_bytes(int batch, int heads, int seq_len, int head_dim,
                                    int causal, int piece_tiles);
 int fa_fwd_split_pieces(int batch, int heads, int seq_len, int head_dim, int causal);
@@ -161,7 +166,7 @@ int fa_fwd_bf16_ws(const void* q, const void* k, const void* v, void* o,
  * fa_config_info): they are not stable across releases (round 3 renumbered
  * 0-49 to 0-43 when the table was trimmed to the dispatched tiers; round 4
  * appended the head_dim-64 W4 configs 44-47; round 5 the paired
- * short-sequence configs 48-51).  Select a tier by its
+ * short-sequence configs 48-51 and their four-block twins 52-55).  Select a tier by its
  * fa_config_info().name, not by a remembered id. */
 int fa_select_config(int batch, int heads, int seq_len, int causal);
 
