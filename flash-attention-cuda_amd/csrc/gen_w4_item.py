@@ -1399,6 +1399,8 @@ def q_scale(st):
         lo = {x: f"v{144 + 3 * (x - x0)}" for x in xs}
         hi = {x: f"v{145 + 3 * (x - x0)}" for x in xs}
         pk = {x: f"v{146 + 3 * (x - x0)}" for x in xs}
+        if "noqscale" in XP:  # timing only (wrong results): Q unscaled, no VALU
+            continue
         if mix():
             for x in xs:
                 for op in mix_pk(pk[x], f"v{x}", f"v{x}", "%[c]", f16src=True):
@@ -1526,9 +1528,10 @@ def prologue(st, causal, split=False):
     st.raw(f"s_mov_b32 {ST1}, {QM}")
     mask_last_tile(st, causal)
     st.label(skip)
-    slow_softmax(st, first=True)
-    for e in exp_ops():
-        st.emit(e)
+    if "nofirst" not in XP:  # timing only (wrong results): no first-tile softmax
+        slow_softmax(st, first=True)
+        for e in exp_ops():
+            st.emit(e)
     prostamp(st, 3)  # -> first softmax + exp2 done
     # V(0), K(1) landed: into their LDS images (warm with the deferred
     # epilogue: its 16 O stores are the youngest, behind stage 0's 8 loads)
@@ -1677,6 +1680,16 @@ def s0_with_epilogue(st):
         for t in range(NT()):
             gaps.setdefault(4 * NT() * cb + 1 + t, []).append(k_read(t, cb + 1, kslot(cb + 1, t), kb))
     ops = epilogue_ops(False, ro=ROSAVE, rowbase=ROWSAVE, zero_o=True)
+    if "noepi" in XP:  # timing only (wrong results): no deferred epilogue at all
+        ops = []
+    # timing only (wrong results): the epilogue without its O stores / with
+    # only its O, l zeroing / without the zeroing
+    if "epinostore" in XP:
+        ops = [o for o in ops if isinstance(o, str) or not o.text.startswith("buffer_store")]
+    if "epizonly" in XP:
+        ops = [o for o in ops if isinstance(o, Ins) and o.text.startswith("v_accvgpr_write")]
+    if "epinozero" in XP:
+        ops = [o for o in ops if isinstance(o, str) or not o.text.startswith("v_accvgpr_write")]
     n = len(mf)
     for i, op in enumerate(ops):
         gaps.setdefault((i * n) // len(ops), []).append(op)
