@@ -90,8 +90,8 @@ V_AHEAD = int(os.environ.get("W4_V_AHEAD", "3"))
 WAGE = int(os.environ.get("W4_WAGE", "8"))
 
 # head_dim of the generated function (set_hd): 128, the reference's, or 64.
-# Q/K/V/O rows are 2*hd bytes in HBM; the LDS images keep 256-B row slots at
-# either (a 64-wide row fills half a slot), as the 8-wave kernels' do
+# Q/K/V/O rows are 2*hd bytes in HBM and in the (packed) LDS tile images:
+# 16 KiB per 64-key tile at 128, 8 KiB at 64 (fa_w4_kernel.hpp k_off64/v_off64)
 HDC = {"hd": 128}
 
 
@@ -1175,7 +1175,21 @@ def body(st, p, causal, labels):
                 st.emit(c)
     pv_plain(st, p)
     st.label(L["end"][p], drain_lgkm=True)
-    if dma():
+    if dma() and "epiwait16" in XP:
+        # timing only (wrong results): iteration 0 after a deferred epilogue
+        # does not wait for the epilogue's 16 O stores (nor, since they are
+        # older, reliably for its own DMA) -- the O stores' ack latency
+        w16, wd = newlabel("w16"), newlabel("wd")
+        st.raw(f"s_cmp_eq_u32 {PEND}, 1")
+        st.branch("s_cbranch_scc1", w16)
+        st.raw("s_waitcnt vmcnt(0)")
+        st.branch("s_branch", wd)
+        st.label(w16)
+        st.raw(f"s_waitcnt vmcnt({nst()})")
+        st.raw(f"s_mov_b32 {PEND}, 0")
+        st.label(wd)
+        st.label(L["end_nowait"][p], drain_lgkm=True)
+    elif dma():
         # this iteration's LDS-DMA landed before the barrier publishes it (the
         # last iteration issues none: its next-item prefetch stays in flight)
         st.raw("s_waitcnt vmcnt(0)")
@@ -1459,6 +1473,8 @@ def prologue(st, causal, split=False):
         for b in range(4):
             st.raw(f"v_mov_b32 {MREF[b]}, 0")
         st.raw(f"s_waitcnt vmcnt({2 * NPASS() + sg0()})")
+        if "epiwait16" in XP:
+            st.raw(f"s_mov_b32 {PEND}, 1")
     else:
         # (older than the previous item's O stores)
         zero_state(st)
@@ -1467,6 +1483,8 @@ def prologue(st, causal, split=False):
     st.branch("s_branch", join)
     # ---- cold: the chunk's first item
     st.label(cold)
+    if "epiwait16" in XP:
+        st.raw(f"s_mov_b32 {PEND}, 0")
     # Q rows qw + 16b + r16: offset (qw + 16b) * 256 + %[qoff]
     st.raw(f"s_lshl_b32 {ST0}, {QW}, {ROWSH()}")
     for b in range(4):
