@@ -535,6 +535,12 @@ static long long persistent_blocks(const Config& cfg, long long bh, int nqb) {
   return 8 * c;
 }
 
+// band of the causal item order at <= 64 heads: 1 = the causal pairs (A/B
+// knob for traffic studies: -DFA_BAND_FEW_HEADS=16 runs the band snake)
+#ifndef FA_BAND_FEW_HEADS
+#define FA_BAND_FEW_HEADS 1
+#endif
+
 static int launch(int id, const void* q, const void* k, const void* v, void* o, int bh,
                   int seq_len, int num_splits, float* part_o, float* part_ml,
                   hipStream_t stream, unsigned* pool_ctr = nullptr) {
@@ -556,7 +562,7 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   p.c = p.scale * 1.4426950408889634f;        // LOG2E, ref :239
   // few heads per XCD: plain heaviest-first balances better; many: keep the
   // query blocks of a head together for L2 reuse (profiles/r01_band_ab.txt)
-  p.band = bh <= 64 ? 1 : 16;
+  p.band = bh <= 64 ? FA_BAND_FEW_HEADS : 16;
   long long blocks = (long long)p.nqb * bh * num_splits;
   if (blocks > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
   if (cfg.kind == 2 || cfg.kind == 5) blocks = persistent_blocks(cfg, bh, p.nqb);
