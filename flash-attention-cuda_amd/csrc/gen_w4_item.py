@@ -1627,7 +1627,15 @@ def epilogue_ops(split, ro=RO, rowbase=ST1, zero_o=False):
             E(vmem(f"buffer_store_dword {T[8]}, {T[10]}, {RL}, 0 offen sc1", r=[T[8], T[10]]))
             E("s_nop 1")
         # row offset: (qw + 16b + r16) * 256 + 2 * dlane
-        E(valu(f"v_add_u32 {T[7]}, {rowbase}, %[ooff]", r=["%[ooff]"], w=[T[7]]))
+        if "epilines" in XP:
+            # timing only (wrong layout): each store one contiguous KiB = 8
+            # whole 128-B lines of the block's rows, lane-linear
+            E(valu(f"v_mbcnt_lo_u32_b32 {T[7]}, -1, 0", w=[T[7]]))
+            E(valu(f"v_mbcnt_hi_u32_b32 {T[7]}, -1, {T[7]}", r=[T[7]], w=[T[7]]))
+            E(valu(f"v_lshlrev_b32 {T[7]}, 4, {T[7]}", r=[T[7]], w=[T[7]]))
+            E(valu(f"v_add_u32 {T[7]}, {rowbase}, {T[7]}", r=[T[7]], w=[T[7]]))
+        else:
+            E(valu(f"v_add_u32 {T[7]}, {rowbase}, %[ooff]", r=["%[ooff]"], w=[T[7]]))
         if b:
             E(valu(f"v_add_u32 {T[7]}, {16 * ROWB() * b}, {T[7]}", r=[T[7]], w=[T[7]]))
         for ep in range(NE() // 2):
@@ -1657,7 +1665,8 @@ def epilogue_ops(split, ro=RO, rowbase=ST1, zero_o=False):
             for dw in range(2):
                 E(valu(f"v_permlane16_swap_b32 {X[dw]}, {Y[dw]}", r=[X[dw], Y[dw]], w=[X[dw], Y[dw]]))
             pol = OPOL if not split else " sc1"
-            E(vmem(f"buffer_store_dwordx4 v[152:155], {T[7]}, {ro}, 0 offen offset:{64 * ep}{pol}",
+            E(vmem(f"buffer_store_dwordx4 v[152:155], {T[7]}, {ro}, 0 offen "
+                   f"offset:{(1024 if 'epilines' in XP else 64) * ep}{pol}",
                    r=["v[152:155]", T[7]]))
             # (no pad: the next write of v[152:155] is the next pair's
             # conversion, 20+ instructions on)

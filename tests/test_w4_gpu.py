@@ -182,9 +182,9 @@ def test_w4_second_item_chunk(b, h, s, causal):
 
 
 # head_dim 64: the same item program with 2-step QK^T chains, 4 O^T column
-# blocks per row block and register-staged K/V (rows of 128 B in HBM, the
-# images' 256-B slots half filled); against the head_dim-64 persistent
-# ping-pong (same arithmetic) and the oracle
+# blocks per row block, K/V by LDS-DMA into packed 128-B-row images (round
+# 5; register-staged into half-filled 256-B slots before); against the
+# head_dim-64 persistent ping-pong (same arithmetic) and the oracle
 D64_W4 = "d64_" + W4
 D64_BASE = "d64_bm256_bn64_w8_m16_pingpong_persistent"
 D64_SHAPES = [(1, 8, 512), (2, 64, 2048), (3, 40, 1000), (1, 203, 300), (4, 50, 64), (1, 7, 4096),
@@ -233,5 +233,48 @@ def test_w4_d64_bf16(shape, causal):
     sc = q.float() @ k.float().transpose(-1, -2) / 64 ** 0.5
     if causal:
         sc = sc + torch.full((s, s), float("-inf"), device="cuda").triu(1)
+    ref = torch.softmax(sc, -1) @ v.float()
+    assert (out.float() - ref).abs().max().item() <= 5e-3
+
+
+BF16_D64_BASE = "bf16_d64_bm256_bn64_w8_m16_pingpong_persistent"
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", [(1, 8, 512), (3, 40, 1000), (2, 64, 2048), (1, 4, 77), (1, 2, 8192),
+                                   (2100, 32, 64)], ids=lambda s: "x".join(map(str, s)))
+def test_w4_d64_bf16_matches_pingpong(shape, causal):
+    """bf16 at head_dim 64 (the packed-image LDS-DMA program on the bf16
+    MFMA) against the bf16 head_dim-64 persistent ping-pong -- the same
+    arithmetic up to O's final rounding, within two bf16 ulps at |O| < 0.5
+    (the ping-pong's short non-causal tail runs as KV-pair halves) -- and
+    the fp32 torch reference at 5e-3; a long head and a second item chunk
+    (2100 x 32 heads of 64 rows: > 256 items per workgroup) included"""
+    fa = _fa()
+    b, h, s = shape
+    q, k, v = (_rand((b, h, s, 64), 1400 + i).to(torch.bfloat16) for i in range(3))
+    base = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(BF16_D64_BASE)[causal])
+    out = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids("bf16_" + D64_W4)[causal])
+    torch.cuda.synchronize()
+    assert out.dtype == torch.bfloat16
+    assert (out.float() - base.float()).abs().max().item() <= 2.0 ** -8
+    for bi in range(min(b, 2)):
+        sc = q[bi].float() @ k[bi].float().transpose(-1, -2) / 64 ** 0.5
+        if causal:
+            sc = sc + torch.full((s, s), float("-inf"), device="cuda").triu(1)
+        ref = torch.softmax(sc, -1) @ v[bi].float()
+        assert (out[bi].float() - ref).abs().max().item() <= 5e-3
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_w4_d64_bf16_peaked(causal):
+    fa = _fa()
+    q, k = (_rand((1, 8, 1000, 64), 1450 + i, scale=4.0).to(torch.bfloat16) for i in range(2))
+    v = _rand((1, 8, 1000, 64), 1452).to(torch.bfloat16)
+    out = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids("bf16_" + D64_W4)[causal])
+    torch.cuda.synchronize()
+    sc = q.float() @ k.float().transpose(-1, -2) / 64 ** 0.5
+    if causal:
+        sc = sc + torch.full((1000, 1000), float("-inf"), device="cuda").triu(1)
     ref = torch.softmax(sc, -1) @ v.float()
     assert (out.float() - ref).abs().max().item() <= 5e-3
