@@ -353,9 +353,9 @@ constexpr kernel_fn pick_kernel() {
   if constexpr (KIND == 5)
     return fa_fwd_f16_w4_kernel<(C != 0), DT == 1, HDIM>;
   else if constexpr (KIND == 6)
-    return fa_fwd_w4p_kernel<(C != 0), DT == 1, 1>;
+    return fa_fwd_w4p_kernel<(C != 0), DT == 1, 1, HDIM>;
   else if constexpr (KIND == 7)
-    return fa_fwd_w4p_kernel<(C != 0), DT == 1, 2>;
+    return fa_fwd_w4p_kernel<(C != 0), DT == 1, 2, HDIM>;
 
   else if constexpr (KIND == 3)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
@@ -398,9 +398,10 @@ constexpr kernel_fn pick_kernel() {
 #define FA_CFG_W4(ID, C, DT, NAME) FA_CFG_W4D(ID, C, DT, 128, NAME)
 // W4P: 4 waves x 16 query rows of each of two (G = 1) or four (G = 2) 64-row
 // blocks, K/V double-buffered (64 KB)
-#define FA_CFG_W4P(ID, G, C, DT, NAME)                                                 \
-  {{ID, 128 * (G), 64, 4, C, 0, kW4PLdsBytes, NAME, DT, 128}, 0, 5 + (G),                \
-   pick_kernel<4, 64, C, 5 + (G), 0, DT, 128>()}
+#define FA_CFG_W4PD(ID, G, C, DT, HDIM, NAME)                                          \
+  {{ID, 128 * (G), 64, 4, C, 0, kW4PLdsBytes, NAME, DT, HDIM}, 0, 5 + (G),               \
+   pick_kernel<4, 64, C, 5 + (G), 0, DT, HDIM>()}
+#define FA_CFG_W4P(ID, G, C, DT, NAME) FA_CFG_W4PD(ID, G, C, DT, 128, NAME)
 
 // Only tiers the dispatcher picks, explicit entry points (split-KV) and the
 // baselines a test compares against (the per-item ping-pong 2/3: the
@@ -471,6 +472,16 @@ static const Config kConfigs[] = {
     FA_CFG_W4P(53, 2, 1, 0, "bm256_bn64_w4x64_m16_asm_quad_causal"),
     FA_CFG_W4P(54, 2, 0, 1, "bf16_bm256_bn64_w4x64_m16_asm_quad_noncausal"),
     FA_CFG_W4P(55, 2, 1, 1, "bf16_bm256_bn64_w4x64_m16_asm_quad_causal"),
+    // their head_dim-64 twins (round 5: the generator's set_hd, W4's packed
+    // 128-B-row images)
+    FA_CFG_W4PD(56, 1, 0, 0, 64, "d64_bm128_bn64_w4x32_m16_asm_pair_noncausal"),
+    FA_CFG_W4PD(57, 1, 1, 0, 64, "d64_bm128_bn64_w4x32_m16_asm_pair_causal"),
+    FA_CFG_W4PD(58, 1, 0, 1, 64, "bf16_d64_bm128_bn64_w4x32_m16_asm_pair_noncausal"),
+    FA_CFG_W4PD(59, 1, 1, 1, 64, "bf16_d64_bm128_bn64_w4x32_m16_asm_pair_causal"),
+    FA_CFG_W4PD(60, 2, 0, 0, 64, "d64_bm256_bn64_w4x64_m16_asm_quad_noncausal"),
+    FA_CFG_W4PD(61, 2, 1, 0, 64, "d64_bm256_bn64_w4x64_m16_asm_quad_causal"),
+    FA_CFG_W4PD(62, 2, 0, 1, 64, "bf16_d64_bm256_bn64_w4x64_m16_asm_quad_noncausal"),
+    FA_CFG_W4PD(63, 2, 1, 1, 64, "bf16_d64_bm256_bn64_w4x64_m16_asm_quad_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 

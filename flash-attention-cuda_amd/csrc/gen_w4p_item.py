@@ -43,10 +43,21 @@ import gen_w4_item as w4  # noqa: E402
 from gen_w4_item import DT, NINF, R, Stream, dsr, mfma, salu, set_dtype, valu, vmem  # noqa: E402
 
 NB = 4                 # query blocks per workgroup (at most)
-NT, NE = 4, 8          # head_dim 128: k-steps of a QK^T chain, 16-column O blocks
-ROWB = 256             # bytes of a Q/K/V/O row
-TILEB = 64 * ROWB      # a 64-key K or V tile
-PASSL = 4096           # LDS stride of a staging pass
+# head_dim of the generated function (set_hd: 128, the reference's, or 64):
+# k-steps of a QK^T chain, 16-column O blocks, bytes of a Q/K/V/O row (HBM
+# and the packed LDS images), of a 64-key tile, 1-KiB LDS-DMA pieces per wave
+# and tensor, row shift
+NT, NE, ROWB, TILEB, NPIECE, ROWSH = 4, 8, 256, 16384, 4, 8
+PASSL = 4096           # LDS stride of a 4-KiB staging pass (32 rows at 64, 16 at 128)
+
+
+def set_hd(hd):
+    global NT, NE, ROWB, TILEB, NPIECE, ROWSH
+    NT, NE, ROWB = hd // 32, hd // 16, 2 * hd
+    TILEB = 64 * ROWB
+    NPIECE = TILEB // 4096
+    ROWSH = 8 if hd == 128 else 7
+    w4.set_hd(hd)
 RESCALE = "0x41000000"  # 8.0: m_ref moves when a row max grew past it (log2 units)
 
 # ---------------------------------------------------------------------------
@@ -146,7 +157,10 @@ KVH = [f"%[kvh{b}]" for b in range(NB)]
 TB = [f"%[t{b}]" for b in range(NB)]
 
 MAX_OFF, LEFT_OFF, DEC_GAP = 2, 3, 6
-LAG = 2
+
+
+def lag():  # chains between a chain and its maxima (a chain is NT MFMAs)
+    return 2 if NT == 4 else 3
 
 # diagnostic builds only (never the product library; tools/w4_variant.sh):
 # W4P_DIAG=stamps accumulates per wave the shader cycles of the prologue, of
@@ -192,26 +206,33 @@ def stamp_path_end(st):
 
 def vahead(np_):
     """V^T fragments read ahead of their PV MFMAs: >= 8 MFMAs of cover for the
-    LDS latency"""
-    return {1: 6, 2: 4}.get(np_, 3)
+    LDS latency (at head_dim 64 at most the tile's 8)"""
+    return min({1: 6, 2: 4}.get(np_, 3), 2 * NE)
 
 
 def kslot(cb, t):
-    return 4 * (cb & 1) + t
+    """K fragment slot: two 16-key blocks' fragments at head_dim 128 (read one
+    block ahead), the whole tile's 8 at 64"""
+    return 4 * (cb & 1) + t if NT == 4 else 2 * cb + t
 
 
 def k_read(t, cb, kb):
     s = kslot(cb, t)
-    return dsr(f"ds_read_b128 {KF(s)}, {KADDR[t]} offset:{kb + 4096 * cb}", KF(s), KADDR[t])
+    return dsr(f"ds_read_b128 {KF(s)}, {KADDR[t]} offset:{kb + 16 * ROWB * cb}", KF(s), KADDR[t])
+
+
+def k_reads_tile(kb):
+    """head_dim 64: every K fragment of the tile at once (the 8 slots hold it)"""
+    return [k_read(t, cb, kb) for cb in range(4) for t in range(NT)]
 
 
 def v_reads(f, vb):
     u, e = divmod(f, NE)
     slot = f % 8
-    off = vb + 8192 * u + 512 * (e >> 1)
+    off = vb + 32 * ROWB * u + 512 * (e >> 1)
     a = VADDR[e & 1]
     return [dsr(f"ds_read_b64_tr_b16 {VF(slot, 0)}, {a} offset:{off}", VF(slot, 0), a),
-            dsr(f"ds_read_b64_tr_b16 {VF(slot, 1)}, {a} offset:{off + 4096}", VF(slot, 1), a)]
+            dsr(f"ds_read_b64_tr_b16 {VF(slot, 1)}, {a} offset:{off + 16 * ROWB}", VF(slot, 1), a)]
 
 
 def qk_chain(b, cb):
@@ -260,16 +281,17 @@ def dma_pieces(p):
     """LDS-DMA of K(j+2) -> kbuf[p], V(j+1) -> vbuf[1-p]: (M0 set, load)
     pairs, then the descriptors advance one tile (gen_w4_item.dma_loads)"""
     pairs = []
-    for i in range(4):
+    for i in range(NPIECE):
         pairs.append((salu(f"s_add_u32 m0, %[dmab], {KBUF[p] + 1024 * i}"),
                       vmem(f"buffer_load_dwordx4 {KD(i)}, {SK}, 0 offen lds", r=[KD(i)])))
-    for i in range(4):
+    for i in range(NPIECE):
         pairs.append((salu(f"s_add_u32 m0, %[dmab], {VBUF[1 - p] + 1024 * i}"),
                       vmem(f"buffer_load_dwordx4 {VD(i)}, {SV}, 0 offen lds", r=[VD(i)])))
-    adv = [[salu("s_add_u32 s40, s40, 0x4000"), salu("s_addc_u32 s41, s41, 0")],
-           [salu(f"s_sub_i32 {SKREM}, {SKREM}, 0x4000"), salu(f"s_max_i32 s42, {SKREM}, 0")],
-           [salu("s_add_u32 s44, s44, 0x4000"), salu("s_addc_u32 s45, s45, 0")],
-           [salu(f"s_sub_i32 {SVREM}, {SVREM}, 0x4000"), salu(f"s_max_i32 s46, {SVREM}, 0")]]
+    tb = hex(TILEB)
+    adv = [[salu(f"s_add_u32 s40, s40, {tb}"), salu("s_addc_u32 s41, s41, 0")],
+           [salu(f"s_sub_i32 {SKREM}, {SKREM}, {tb}"), salu(f"s_max_i32 s42, {SKREM}, 0")],
+           [salu(f"s_add_u32 s44, s44, {tb}"), salu("s_addc_u32 s45, s45, 0")],
+           [salu(f"s_sub_i32 {SVREM}, {SVREM}, {tb}"), salu(f"s_max_i32 s46, {SVREM}, 0")]]
     return pairs, adv
 
 
@@ -303,7 +325,7 @@ def phase_a(st, p, nq, np_):
     def put(k, ins):
         gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
 
-    put(0, [k_read(t, 0, kb) for t in range(NT)])
+    put(0, [k_read(t, 0, kb) for t in range(NT)] if NT == 4 else k_reads_tile(kb))
     for x, (b, cb) in enumerate(chains):
         c = cvt_block(b, cb)
         if cb == 0:
@@ -311,13 +333,13 @@ def phase_a(st, p, nq, np_):
         else:
             put(NT * x - 1, c[0])
             put(NT * x, c[1])
-        if b == 0 and cb < 3:
+        if b == 0 and cb < 3 and NT == 4:
             for t in range(NT):
                 put(NT * x + 1 + t % 3, k_read(t, cb + 1, kb))
-        if x >= LAG:
-            by, cby = chains[x - LAG]
+        if x >= lag():
+            by, cby = chains[x - lag()]
             mm = max_block(by, cby, first=(cby == 0))
-            put(NT * x + MAX_OFF, mm[0])
+            put(min(NT * x + MAX_OFF, n), mm[0])
             put(min(NT * x + MAX_OFF + 1, n), mm[1])
     # conversions of the blocks with a PV(j) but no QK(j+1) (their drain): any gap
     extra = [c for b in range(nq, np_) for cb in range(4) for c in cvt_block(b, cb)]
@@ -332,15 +354,15 @@ def phase_a(st, p, nq, np_):
         put(a0 + sp * i + 1, ld)
     g = a0 + sp * (len(pairs) - 1) + 2
     for i, ins in enumerate(adv):
-        put(g + i, ins)
+        put(min(g + i, n), ins)
     # the first V^T fragments of PV(j) (V(j) is ready since the last barrier)
     for f in range(va):
         for i, r in enumerate(v_reads(f, VBUF[p])):
-            put(max(0, n - 2 * va) + 2 * f + i, r)
+            put(min(max(0, n - 2 * va) + 2 * f + i, n), r)
     assert max(gaps) <= n, "every filler lands in a gap"
     st.interleave(mf, gaps)
     left = []
-    for y in range(len(chains) - LAG, len(chains)):
+    for y in range(max(0, len(chains) - lag()), len(chains)):
         by, cby = chains[y]
         left += max_block(by, cby, first=False)
     return left
@@ -387,9 +409,11 @@ def phase_b(st, p, nq, np_, leftover, label_slow, label_end):
         r = v_reads(f, vb)
         put(k + 1, r[0])
         put(k + 2, r[1])
-    for i, ins in enumerate(leftover):
-        put(LEFT_OFF + i, ins)
-    assert not leftover or LEFT_OFF + len(leftover) - 1 <= DEC_GAP
+    # (head_dim 64: three chains' maxima, two per gap)
+    lo = [LEFT_OFF + (i if NT == 4 else i // 2) for i in range(len(leftover))]
+    for k, ins in zip(lo, leftover):
+        put(k, ins)
+    assert not leftover or lo[-1] <= DEC_GAP
     if nq == 0:
         st.interleave(mf, gaps)
         st.branch("s_branch", label_end)
@@ -525,11 +549,12 @@ def full_max(st, b):
 
 def qk_plain(st, kb, nb):
     """QK^T of one tile for blocks 0..nb-1, not interleaved (prologue): each
-    16-key block's four K fragments read one block ahead"""
-    for t in range(NT):
-        st.emit(k_read(t, 0, kb))
+    16-key block's four K fragments read one block ahead (head_dim 64: the
+    whole tile's at once)"""
+    for r in ([k_read(t, 0, kb) for t in range(NT)] if NT == 4 else k_reads_tile(kb)):
+        st.emit(r)
     for cb in range(4):
-        if cb < 3:
+        if cb < 3 and NT == 4:
             for t in range(NT):
                 st.emit(k_read(t, cb + 1, kb))
         for b in range(nb):
@@ -566,11 +591,12 @@ def rsrc(st, dst, lo, hi, records):
 def q_scale(st):
     """Q * c (fp32 product, then fp16: M16::scale_q) from v0-63 into a144-207,
     eight elements at a time in the (free) V^T fragment registers"""
-    for x0 in range(0, 16 * NB, 8):
-        xs = range(x0, x0 + 8)
-        lo = {x: f"v{144 + 3 * (x - x0)}" for x in xs}
-        hi = {x: f"v{145 + 3 * (x - x0)}" for x in xs}
-        pk = {x: f"v{146 + 3 * (x - x0)}" for x in xs}
+    qregs = [16 * b + j for b in range(NB) for j in range(4 * NT)]  # Q(b, t) raw: v[16b + 4t ..]
+    for c0 in range(0, len(qregs), 8):
+        xs = qregs[c0:c0 + 8]
+        lo = {x: f"v{144 + 3 * i}" for i, x in enumerate(xs)}
+        hi = {x: f"v{145 + 3 * i}" for i, x in enumerate(xs)}
+        pk = {x: f"v{146 + 3 * i}" for i, x in enumerate(xs)}
         if w4.mix():  # one rounding: gen_w4_item.mix_pk
             for x in xs:
                 for op in w4.mix_pk(pk[x], f"v{x}", f"v{x}", "%[c]", f16src=True):
@@ -606,14 +632,21 @@ def prologue(st, causal):
     st.raw(f"s_mov_b32 {SM0}, m0")
     st.raw(f"v_mov_b32 {KD(0)}, %[kdma]")
     st.raw(f"v_mov_b32 {VD(0)}, %[vdma]")
+    # DMA piece i's sources (gen_w4_item.dma_setup: head_dim 128 / 64)
     for i in range(1, 4):
-        st.raw(f"v_add_u32 {KD(i)}, {1024 * i}, %[kdma]")
-        st.raw(f"v_xor_b32 {KD(i)}, {64 * i}, {KD(i)}")
-        st.raw(f"v_add_u32 {VD(i)}, {2048 * (i >> 1) + 128 * (i & 1)}, %[vdma]")
-        if i >= 2:
+        if i < NPIECE:
+            st.raw(f"v_add_u32 {KD(i)}, {1024 * i}, %[kdma]")
+            st.raw(f"v_xor_b32 {KD(i)}, {64 * i}, {KD(i)}")
+        if i < NPIECE and NT == 2:
+            st.raw(f"v_add_u32 {VD(i)}, 1024, %[vdma]")
             st.raw(f"v_xor_b32 {VD(i)}, 32, {VD(i)}")
-        st.raw(f"v_add_u32 {KOFF[i]}, {4096 * i}, %[koff]")
-        st.raw(f"v_add_u32 {VOFF[i]}, {4096 * i}, %[voff]")
+        elif i < NPIECE:
+            st.raw(f"v_add_u32 {VD(i)}, {2048 * (i >> 1) + 128 * (i & 1)}, %[vdma]")
+            if i >= 2:
+                st.raw(f"v_xor_b32 {VD(i)}, 32, {VD(i)}")
+        if i < NPIECE:
+            st.raw(f"v_add_u32 {KOFF[i]}, {4096 * i}, %[koff]")
+            st.raw(f"v_add_u32 {VOFF[i]}, {4096 * i}, %[voff]")
     st.raw(f"v_mov_b32 {VNINF}, {NINF}")
     for i in range(4):
         st.raw(f"v_mov_b32 v{184 + i}, {DT['one2']}")
@@ -623,19 +656,19 @@ def prologue(st, causal):
     rsrc(st, 60, "%[olo]", "%[ohi]", "%[qrec]")
     # Q rows qr_b + r16, chunk g of k-step t: (qr_b << 8) + qoff + 64 t
     for b in range(NB):
-        st.raw(f"s_lshl_b32 {ST0}, {QR[b]}, 8")
+        st.raw(f"s_lshl_b32 {ST0}, {QR[b]}, {ROWSH}")
         st.raw(f"v_add_u32 {T[b]}, {ST0}, %[qoff]")
-    for i in range(4):
+    for i in range(NPIECE):
         st.raw(f"v_add_u32 {T[4 + i]}, {hex(TILEB)}, {KOFF[i]}")
     st.nop(5)
     for b in range(NB):
         for t in range(NT):
             st.raw(f"buffer_load_dwordx4 {R('v', 16 * b + 4 * t, 4)}, {T[b]}, {RQ}, 0 offen offset:{64 * t}")
-    for i in range(4):
+    for i in range(NPIECE):
         st.raw(f"buffer_load_dwordx4 {KF(i)}, {KOFF[i]}, {SK}, 0 offen")
-    for i in range(4):
+    for i in range(NPIECE):
         st.raw(f"buffer_load_dwordx4 {VST1(i)}, {VOFF[i]}, {SV}, 0 offen")
-    for i in range(4):
+    for i in range(NPIECE):
         st.raw(f"buffer_load_dwordx4 {KST1(i)}, {T[4 + i]}, {SK}, 0 offen")
     # DMA descriptors start at K(2) / V(1)
     t2, t1 = hex(2 * TILEB), hex(TILEB)
@@ -654,13 +687,13 @@ def prologue(st, causal):
         st.raw(f"v_mov_b32 v{x}, 0")
     for b in range(NB):
         st.raw(f"v_mov_b32 {MREF[b]}, 0")
-    # Q (16) and K(0) (4) landed; V(0), K(1) (8) may still fly
-    st.raw("s_waitcnt vmcnt(8)")
-    for i in range(4):
+    # Q and K(0) landed; V(0), K(1) may still fly
+    st.raw(f"s_waitcnt vmcnt({2 * NPIECE})")
+    for i in range(NPIECE):
         st.raw(f"ds_write_b128 %[klds], {KF(i)} offset:{KBUF[0] + PASSL * i}")
     q_scale(st)
     st.raw("s_waitcnt vmcnt(0)")
-    for i in range(4):
+    for i in range(NPIECE):
         st.raw(f"ds_write_b128 %[vlds], {VST1(i)} offset:{VBUF[0] + PASSL * i}")
         st.raw(f"ds_write_b128 %[klds], {KST1(i)} offset:{KBUF[1] + PASSL * i}")
     st.raw("s_waitcnt lgkmcnt(0)")
@@ -713,7 +746,7 @@ def epilogue_block(st, b):
     """O / l -> fp16 rows qr_b + r16 (M16::store_o: permlane16 swaps, dwordx4
     stores, sc1)"""
     l, inv = T[0], T[1]
-    st.raw(f"s_lshl_b32 {ST1}, {QR[b]}, 8")
+    st.raw(f"s_lshl_b32 {ST1}, {QR[b]}, {ROWSH}")
     st.emit(valu(f"v_accvgpr_read_b32 {l}, {L(b, 0)}", r=[L(b, 0)], w=[l]))
     # inv = l > 0 ? 1.0f / l : 0  (IEEE division, the compiler's sequence)
     st.emit(valu(f"v_div_scale_f32 {T[2]}, {DIVS}, {l}, {l}, 1.0", r=[l], w=[T[2]]))
@@ -820,7 +853,7 @@ def generate(causal):
         st.raw("s_waitcnt vmcnt(0)")
         stamp_now(st, 72)
         st.raw("s_sub_u32 s90, s72, s76")
-        st.raw(f"s_lshl_b32 {ST1}, {QR[0]}, 8")
+        st.raw(f"s_lshl_b32 {ST1}, {QR[0]}, {ROWSH}")
         for i in range(13):
             st.raw(f"v_mov_b32 v{i}, s{78 + i}")
         for i in range(13, 16):
@@ -846,7 +879,8 @@ def cxx(causal, bf16, lines):
     vclob = ", ".join(f'"v{i}"' for i in range(NV))
     aclob = ", ".join(f'"a{i}"' for i in range(NA))
     sclob = ", ".join(f'"s{i}"' for i in range(NS_LO, NS_DIAG if STAMPS else NS_HI))
-    name = ("w4p_item_causal" if causal else "w4p_item_noncausal") + ("_bf16" if bf16 else "_f16")
+    name = (("w4p_item_causal" if causal else "w4p_item_noncausal") + ("_d64" if NT == 2 else "")
+            + ("_bf16" if bf16 else "_f16"))
     blocks = ",\n        ".join(f'[qr{b}] "s"(rn.qr[{b}]), [kvh{b}] "s"(rn.kvh[{b}]), [t{b}] "s"(rn.t[{b}])'
                                  for b in range(NB))
     return f"""
@@ -873,12 +907,15 @@ __device__ __forceinline__ void {name}(const W4PRun& rn, const W4Lane& ln) {{
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else "fa_w4p_item.inc"
     text = HEADER
-    for bf16 in (False, True):
-        set_dtype(bf16)
-        for causal in (False, True):
-            w4._lbl[0] = 0
-            text += cxx(causal, bf16, generate(causal))
+    for hd in (128, 64):
+        set_hd(hd)
+        for bf16 in (False, True):
+            set_dtype(bf16)
+            for causal in (False, True):
+                w4._lbl[0] = 0
+                text += cxx(causal, bf16, generate(causal))
     set_dtype(False)
+    set_hd(128)
     with open(out, "w") as f:
         f.write(text)
 

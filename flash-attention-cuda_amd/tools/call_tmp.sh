@@ -1,16 +1,22 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_w4_gpu.py -m gpu -x -q -k "d64_bf16" --timeout 120 --timeout-method thread > gpurun_out/r05_pytest_d64_bf16.log 2>&1 || { tail -30 gpurun_out/r05_pytest_d64_bf16.log; exit 1; }
-tail -2 gpurun_out/r05_pytest_d64_bf16.log
-AB="timeout -k 10 400 python flash-attention-cuda_amd/tools/ab.py --configs static --libs ,eplines"
-O=gpurun_out/r05_ab_seam_probes4.jsonl
-$AB --seq 4096 --batch 64 --causal --rounds 7 --iters 10 > $O &&
-$AB --seq 8192 --causal --rounds 9 --iters 20 >> $O || exit 1
-cat $O
-AB2="timeout -k 10 400 python flash-attention-cuda_amd/tools/ab.py --dtype bf16 --head-dim 64"
-O2=gpurun_out/r05_ab_w4_d64_bf16.jsonl
-$AB2 --configs 47,19 --seq 4096 --batch 64 --causal --rounds 7 --iters 10 > $O2 &&
-$AB2 --configs 47,19 --seq 8192 --causal --rounds 9 --iters 20 >> $O2 &&
-$AB2 --configs 46,18 --seq 8192 --rounds 9 --iters 20 >> $O2 || exit 1
-cat $O2
+timeout -k 10 900 python -u -m pytest tests/test_w4p_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r05_pytest_w4p_d64.log 2>&1 || { tail -40 gpurun_out/r05_pytest_w4p_d64.log; exit 1; }
+tail -2 gpurun_out/r05_pytest_w4p_d64.log
+AB="timeout -k 10 300 python flash-attention-cuda_amd/tools/ab.py --head-dim 64 --rounds 7 --iters 40"
+O=gpurun_out/r05_ab_w4p_d64.jsonl
+: > $O
+for sh in "1 32 1024" "1 32 2048" "1 32 512" "2 32 1024" "1 8 4096" "1 16 4096" "4 32 1024" "1 32 4096"; do
+  set -- $sh
+  $AB --configs 57,61,auto --batch $1 --heads $2 --seq $3 --causal >> $O || exit 1
+done
+for sh in "1 16 2048" "1 4 8192" "1 32 1024" "1 48 512" "1 32 2048"; do
+  set -- $sh
+  $AB --configs 56,60,auto --batch $1 --heads $2 --seq $3 >> $O || exit 1
+done
+python - <<'PY'
+import json
+for l in open("gpurun_out/r05_ab_w4p_d64.jsonl"):
+    if l.startswith("{"):
+        d = json.loads(l); print(d["batch"], d["heads"], d["seq"], d["causal"], d["config"][:40], d["median_tflops"])
+PY

@@ -63,10 +63,11 @@ def _torch_ref(q, k, v, causal):
     return out
 
 
-def _check(b, h, s, causal, seed, scale=1.0, dtype=torch.float16, oracle_heads=True, tier=PAIR):
+def _check(b, h, s, causal, seed, scale=1.0, dtype=torch.float16, oracle_heads=True, tier=PAIR, d=128):
     fa = _fa()
-    pre = tier if dtype == torch.float16 else "bf16_" + tier
-    q, k, v = (_rand((b, h, s, 128), seed + i, scale if i < 2 else 1.0, dtype) for i in range(3))
+    pre = ("d64_" if d == 64 else "") + tier
+    pre = pre if dtype == torch.float16 else "bf16_" + pre
+    q, k, v = (_rand((b, h, s, d), seed + i, scale if i < 2 else 1.0, dtype) for i in range(3))
     out = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(pre)[causal])
     torch.cuda.synchronize()
     assert torch.isfinite(out.float()).all()
@@ -200,3 +201,46 @@ def test_quad_matches_pair_causal_row0_and_ones():
     ones = torch.ones_like(v)
     o1 = fa.flash_attention_fwd(q, k, ones, causal=True, config=_ids(QUAD)[True])
     assert torch.equal(o1, ones)
+
+
+# head_dim 64 (configs 56-63: the generator's set_hd(64) -- QK^T chains of two
+# k-steps, four O^T column blocks, the whole tile's K fragments read at once,
+# two 1-KiB LDS-DMA pieces per wave and tensor into W4's packed 128-B-row
+# images)
+D64_SHAPES = [(1, 32, 1024), (1, 8, 1000), (2, 3, 320), (1, 4, 64), (1, 2, 65), (1, 1, 130),
+              (1, 16, 2048), (3, 40, 777), (4, 32, 512)]
+
+
+@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", D64_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_pair_d64_matches_oracle(shape, causal, tier):
+    _check(*shape, causal, seed=800, tier=tier, d=64)
+
+
+@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("s", [256, 1000, 2048])
+def test_pair_d64_peaked_rescale(s, causal, tier):
+    _check(1, 8, s, causal, seed=810, scale=4.0, tier=tier, d=64)
+
+
+@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", [(1, 32, 1024), (1, 8, 1000), (2, 3, 320)], ids=lambda s: "x".join(map(str, s)))
+def test_pair_d64_bf16(shape, causal, tier):
+    _check(*shape, causal, seed=830, dtype=torch.bfloat16, tier=tier, d=64)
+
+
+def test_pair_d64_row0_ones_deterministic():
+    fa = _fa()
+    q, k, v = (_rand((1, 8, 2048, 64), 840 + i) for i in range(3))
+    for tier in TIERS:
+        ids = _ids("d64_" + tier)
+        a = fa.flash_attention_fwd(q, k, v, causal=True, config=ids[True])
+        b = fa.flash_attention_fwd(q, k, v, causal=True, config=ids[True])
+        assert torch.equal(a, b)
+        assert torch.equal(a[:, :, 0], v[:, :, 0])
+        ones = torch.ones_like(v)
+        for causal in (False, True):
+            assert torch.equal(fa.flash_attention_fwd(q, k, ones, causal=causal, config=ids[causal]), ones)
