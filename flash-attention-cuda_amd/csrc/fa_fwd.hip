@@ -733,7 +733,11 @@ static int launch_auto(int dtype, const void* q, const void* k, const void* v, v
   int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
   if (rc != FA_OK) return rc;
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
-  const int sel = select_tier(batch, heads, seq_len, causal, head_dim == HD);
+  // the paired tier at head_dim 64 only for causal launches: non-causal its
+  // d64 twin trails the KV-pair / W4 d64 (B=1 H=4 S=8192 851 vs 886, H=16
+  // S=2048 722 vs 744); causal it leads (H=32 S=1024 374 vs 301, S=2048 quad
+  // 653 vs 582, B=2 S=1024 502 vs 410; profiles/r05_ab_w4p_d64.jsonl)
+  const int sel = select_tier(batch, heads, seq_len, causal, head_dim == HD || causal);
   // (head_dim 64 of the W4 tier is the same item program with 2-step QK^T
   // chains and 8-KiB packed tiles: +4-9 % over the 8-wave ping-pong at
   // head_dim 64, profiles/r04_ab_w4_d64.jsonl, r05_ab_d64dma.jsonl)

@@ -14,6 +14,12 @@ for sh in "1 16 2048" "1 4 8192" "1 32 1024" "1 48 512" "1 32 2048"; do
   set -- $sh
   $AB --configs 56,60,auto --batch $1 --heads $2 --seq $3 >> $O || exit 1
 done
+# advice r04: d64 at the W4 tier's thresholds (W4 d64 / KV-pair d64 / 8-wave ping-pong d64 / auto)
+for sh in "1 32 2048 --causal 45,27,15" "1 48 2048 --causal 45,27,15" "1 24 2048 --causal 45,27,15" "1 20 2048 44,26,14" "1 10 4096 44,26,14"; do
+  set -- $sh
+  if [ "$4" = "--causal" ]; then C=--causal; CF=$5; else C=; CF=$4; fi
+  $AB --configs $CF,auto --batch $1 --heads $2 --seq $3 $C >> $O || exit 1
+done
 python - <<'PY'
 import json
 for l in open("gpurun_out/r05_ab_w4p_d64.jsonl"):

@@ -159,8 +159,9 @@ int fa_fwd_bf16_ws(const void* q, const void* k, const void* v, void* o,
  * thread's current HIP device (the W4 tier's tail and the paired tier's
  * one-round test size the grid from it, as the launch does; 256 if the
  * query fails).  The tier is the same for fp16 and bf16; fa_fwd_f16 /
- * fa_fwd_bf16 at head_dim 64 run the head_dim-64 twin of this tier, or of
- * the tier below it when this one has none (the paired tier: head_dim 128).
+ * fa_fwd_bf16 at head_dim 64 run the head_dim-64 twin of this tier, except
+ * that non-causal head_dim-64 launches skip the paired tier (its d64 twin
+ * trails the tier below there) and run the tier below it.
  *
  * Config ids are positions in this build's table (fa_num_configs /
  * fa_config_info): they are not stable across releases (round 3 renumbered
