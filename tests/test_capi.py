@@ -421,3 +421,24 @@ def test_generator_variants_generate(tmp_path, env):
     for fn in ("w4_item_noncausal_f16", "w4_item_causal_bf16", "w4_item_causal_split_f16",
                "w4_item_causal_d64_f16"):
         assert f"void {fn}(" in text, fn
+
+
+def test_tail_pool_workspace_sizing():
+    """fa_fwd_ws_bytes asks for the 64-KB counter region exactly where the W4
+    tier runs its cross-XCD tail pool: >= 64 rounds of 256-row items per XCD
+    in the snake order (256 CUs: >= 2048 items per XCD), never on the causal
+    pairs (<= 64 heads) or other tiers -- no launch, no GPU needed."""
+    lib = _fa().load_library()
+    pool = [(64, 32, 4096, 128, 1), (32, 32, 4096, 128, 1), (16, 32, 8192, 128, 0),
+            (64, 32, 4096, 64, 1), (128, 24, 2048, 128, 1)]
+    none = [(16, 32, 4096, 128, 1),   # 32 rounds
+            (1, 32, 8192, 128, 1),    # causal pairs
+            (1, 32, 16384, 128, 1),
+            (8, 32, 4096, 128, 1),    # 16 rounds
+            (1, 32, 1024, 128, 1),    # the paired short tier
+            (64, 32, 4096, 96, 1)]    # unsupported head_dim
+    for args in pool:
+        assert lib.fa_fwd_ws_bytes(*args, 0) == 65536, args
+        assert lib.fa_fwd_split_pieces(*args) == 0, args
+    for args in none:
+        assert lib.fa_fwd_ws_bytes(*args, 0) == 0, args
