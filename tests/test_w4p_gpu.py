@@ -244,3 +244,27 @@ def test_pair_d64_row0_ones_deterministic():
         ones = torch.ones_like(v)
         for causal in (False, True):
             assert torch.equal(fa.flash_attention_fwd(q, k, ones, causal=causal, config=ids[causal]), ones)
+
+
+@pytest.mark.parametrize("b,h,s,tier", [(1, 8, 4096, "pair"), (1, 16, 4096, "quad"), (2, 32, 1024, "quad")])
+def test_pair_d64_dispatched_long_heads(b, h, s, tier):
+    """head_dim-64 causal launches the dispatcher sends to the W4P twins:
+    sampled rows of every head against fp32 torch, head 0's against the
+    oracle's row-sampled entry"""
+    fa = _fa()
+    q, k, v = (_rand((b, h, s, 64), 860 + i) for i in range(3))
+    out = fa.flash_attention_fwd(q, k, v, causal=True)
+    torch.cuda.synchronize()
+    rows = _sample_rows(s)
+    r = torch.tensor(rows, device=q.device)
+    for bi in range(b):
+        sc = q[bi][:, r].float() @ k[bi].float().transpose(-1, -2) / math.sqrt(64)
+        keep = torch.arange(s, device=q.device)[None, :] <= r[:, None]
+        sc = sc.masked_fill(~keep, float("-inf"))
+        ref = torch.softmax(sc, dim=-1) @ v[bi].float()
+        assert (out[bi][:, r].float() - ref).abs().max().item() <= TOL
+    ro = oracle.attention_rows(_bits(q[0, 0]), _bits(k[0, 0]), _bits(v[0, 0]), rows, True)
+    assert oracle.max_abs_diff(_bits(out[0, 0])[rows], ro) <= TOL
+    # the launch ran the paired tier's d64 twin (the dispatcher's d128 tier name)
+    name = fa.configs()[fa.select_config(b, h, s, True)].name
+    assert f"_asm_{tier}_" in name, name
