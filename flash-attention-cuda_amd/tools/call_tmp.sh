@@ -1,4 +1,8 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_w4p_gpu.py tests/test_capi.py -m gpu -x -v -k "dispatched_long_heads" --timeout 120 --timeout-method thread > gpurun_out/r05_pytest_w4p_d64_long.log 2>&1; rc=$?; tail -8 gpurun_out/r05_pytest_w4p_d64_long.log; exit $rc
+AB="timeout -k 10 300 python flash-attention-cuda_amd/tools/ab.py --configs 49 --libs ,p1nodma,p1nokv --rounds 9 --iters 40"
+O=gpurun_out/r05_ab_w4p_probes.jsonl
+$AB --seq 1024 --causal > $O &&
+$AB --seq 4096 --heads 8 --causal >> $O || exit 1
+cat $O
