@@ -314,7 +314,7 @@ def phase_a(st, p, nq, np_):
         for f in range(va):
             for r in v_reads(f, VBUF[p]):
                 st.emit(r)
-        return []
+        return [], []
     chains = [(b, cb) for cb in range(4) for b in range(nq)]
     mf = []
     for b, cb in chains:
@@ -348,6 +348,15 @@ def phase_a(st, p, nq, np_):
     # LDS-DMA: an M0 write and its load are always an MFMA apart (M0 wait
     # state); two or more blocks spread them over two gaps each, one shares gaps
     pairs, adv = dma_pieces(p)
+    late = []
+    if nq == 1 and np_ == 1 and "p1dmaa" not in w4.XP:
+        # one-block iterations: the V tile's pieces and descriptor advance in
+        # phase B (its buffer is free for the whole iteration) -- eight pieces
+        # at ~60 issue cycles crowd phase A's 16 MFMA gaps; +2.7 % at config 1,
+        # +3.3 % at H=8 S=4096, +0.5-0.9 % elsewhere (profiles/
+        # r05_ab_w4p_dmab.jsonl; W4_XP=p1dmaa keeps them in phase A)
+        late = [ins for pr in pairs[NPIECE:] for ins in pr] + [i for g in adv[2:] for i in g]
+        pairs, adv = pairs[:NPIECE], adv[:2]
     a0, sp = (2, 2) if nq >= 2 else (1, 1)
     for i, (m0, ld) in enumerate(pairs):
         put(a0 + sp * i, m0)
@@ -365,7 +374,7 @@ def phase_a(st, p, nq, np_):
     for y in range(max(0, len(chains) - lag()), len(chains)):
         by, cby = chains[y]
         left += max_block(by, cby, first=False)
-    return left
+    return left, late
 
 
 def mask_pass(st, nq, causal):
@@ -391,7 +400,7 @@ def mask_pass(st, nq, causal):
     st.label(done)
 
 
-def phase_b(st, p, nq, np_, leftover, label_slow, label_end):
+def phase_b(st, p, nq, np_, leftover, label_slow, label_end, late=()):
     """PV(j) of blocks 0..np-1 from vbuf[p]; the rescale decision over the
     blocks 0..nq-1 at DEC_GAP, exp2 of their S(j+1) after it.  nq = 0: the
     PV alone."""
@@ -403,6 +412,9 @@ def phase_b(st, p, nq, np_, leftover, label_slow, label_end):
     def put(k, ins):
         gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
 
+    # phase A's deferred DMA: (M0, load) pairs an MFMA apart, then the advance
+    for i, ins in enumerate(late):
+        put(1 + i, ins)
     va = vahead(np_)
     for f in range(va, 2 * NE):
         k = frag_first[f - va]
@@ -573,9 +585,9 @@ def kname(np_, nq):
 
 def iteration(st, p, np_, nq, causal, Lb):
     stamp_path(st, NB - nq if nq else NPATH - 1)   # 0: 4 QK blocks .. 3: 1; 4: drain
-    left = phase_a(st, p, nq, np_)
+    left, late = phase_a(st, p, nq, np_)
     mask_pass(st, nq, causal)
-    phase_b(st, p, nq, np_, left, Lb["slow_" + kname(np_, nq)][p], Lb["end"][p])
+    phase_b(st, p, nq, np_, left, Lb["slow_" + kname(np_, nq)][p], Lb["end"][p], late)
 
 
 # ---------------------------------------------------------------------------

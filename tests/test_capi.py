@@ -403,7 +403,7 @@ def test_generated_pair_program_is_current(tmp_path):
 @pytest.mark.parametrize("env", [
     {"W4_XP": "rsa"}, {"W4_XP": "cvtearly"}, {"W4_XP": "kpre"}, {"W4_XP": "shift4"},
     {"W4_XP": "nomfz"}, {"W4_XP": "twobar"}, {"W4_WAGE": "0"}, {"W4_V_AHEAD": "5"}, {"W4_DIAG": "stamps"},
-    {"W4_DIAG": "prostamps"}, {"W4_XP": "mix"}, {"W4_XP": "noepi,noqscale,nofirst"}, {"W4_XP": "epinostore"},
+    {"W4_DIAG": "prostamps"}, {"W4_XP": "mix"}, {"W4_XP": "noepi,noqscale,nofirst"}, {"W4_XP": "epinostore"}, {"W4_XP": "p1dmaa"},
 ], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_generator_variants_generate(tmp_path, env):
     """The experiment / diagnostic switches DESIGN.md cites (tools/w4_variant.sh
