@@ -1,7 +1,11 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
+ROUND=r05 bash flash-attention-cuda_amd/tools/gpu_check.sh || exit 1
 bash flash-attention-cuda_amd/tools/vs_sdpa_all.sh || exit 1
 cd flash-attention-cuda_amd
-timeout -k 10 300 python tools/w4_tail.py --seq 4096 --batch 64 --causal > ../gpurun_out/w4_tail.jsonl || exit 1
+for spec in "1 32 1024 --causal" "1 32 2048 --causal --quad"; do
+  set -- $spec
+  timeout -k 10 120 python tools/w4p_stamps.py --batch $1 --heads $2 --seq $3 $4 $5 || exit 1
+done 2>&1 | grep -v amdgpu.ids > ../gpurun_out/w4p_stamps.jsonl || exit 1
 echo done
