@@ -1,8 +1,6 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-ROUND=r05 bash flash-attention-cuda_amd/tools/gpu_check.sh || exit 1
-bash flash-attention-cuda_amd/tools/vs_sdpa_all.sh || exit 1
 cd flash-attention-cuda_amd
 for spec in "1 32 1024 --causal" "1 32 2048 --causal --quad"; do
   set -- $spec
