@@ -251,11 +251,8 @@ def cvt_block(b, cb):
 
 
 def max_block(b, cb, first):
-    return max_at(RMAX[b], 16 * b + 4 * cb, first)
-
-
-def max_at(m, s, first):
-    """running max m over the four scores v[s .. s+3] (first: starts it)"""
+    s = 16 * b + 4 * cb
+    m = RMAX[b]
     if first:
         return [valu(f"v_max3_f32 {m}, v{s}, v{s + 1}, v{s + 2}", r=[f"v{s}", f"v{s + 1}", f"v{s + 2}"], w=[m]),
                 valu(f"v_max_f32 {m}, {m}, v{s + 3}", r=[m, f"v{s + 3}"], w=[m])]
@@ -443,18 +440,9 @@ def phase_b(st, p, nq, np_, leftover, label_slow, label_end, late=()):
             dec.append(valu(f"v_max_f32 {T[0]}, {T[0]}, {RMAX[3]}", r=[T[0], RMAX[3]], w=[T[0]]))
     dec.append(valu(f"v_cmp_lt_f32 vcc, {RESCALE}, {m}", r=[m]))
     exs = [e for b in range(nq) for e in exp_ops(b)]
-    emit_b(st, mf, gaps, dec, exs, lambda: slow_softmax(st, range(nq), first=False),
-           label_slow, label_end)
-
-
-def emit_b(st, mf, gaps, dec, exs, slow, label_slow, label_end):
-    """phase B's emission: the MFMAs with their fillers, the rescale decision
-    dec after gap DEC_GAP, the exp2s exs spread over the later gaps; the slow
-    path (slow(), then the exp2s) behind the decision's branch"""
-    n = len(mf)
     n_g = n - DEC_GAP
     for i, e in enumerate(exs):
-        gaps.setdefault(DEC_GAP + 1 + (i * n_g) // len(exs), []).append(e)
+        put(DEC_GAP + 1 + (i * n_g) // len(exs), e)
     for k in range(DEC_GAP):
         for f in gaps.get(k, []):
             st.emit(f)
@@ -483,7 +471,7 @@ def emit_b(st, mf, gaps, dec, exs, slow, label_slow, label_end):
     for f in gaps.get(n, []):
         if isinstance(f, str) or f.kind != "trans":
             st.emit(f)
-    slow()
+    slow_softmax(st, range(nq), first=False)
     for e in exs:
         st.emit(e)
     st.branch("s_branch", label_end)
@@ -512,16 +500,11 @@ def slow_softmax(st, blocks, first):
 
 
 def row_max_b(st, b, dst):
-    row_max_regs(st, [f"v{16 * b + i}" for i in range(16)], dst)
-
-
-def row_max_regs(st, s, dst):
-    """dst = the row's max over the score registers s (16 or 8) and the 4 lanes of the row"""
-    n = len(s)
+    s = [f"v{16 * b + i}" for i in range(16)]
     st.emit(valu(f"v_max3_f32 {dst}, {s[0]}, {s[1]}, {s[2]}", r=s[0:3], w=[dst]))
-    for i in range(3, n - 1, 2):
+    for i in range(3, 15, 2):
         st.emit(valu(f"v_max3_f32 {dst}, {dst}, {s[i]}, {s[i + 1]}", r=[dst, s[i], s[i + 1]], w=[dst]))
-    st.emit(valu(f"v_max_f32 {dst}, {dst}, {s[n - 1]}", r=[dst, s[n - 1]], w=[dst]))
+    st.emit(valu(f"v_max_f32 {dst}, {dst}, {s[15]}", r=[dst, s[15]], w=[dst]))
     tmp = T[10]
     for sw in ("v_permlane16_swap_b32", "v_permlane32_swap_b32"):
         st.emit(valu(f"v_mov_b32 {tmp}, {dst}", r=[dst], w=[tmp]))
@@ -531,42 +514,30 @@ def row_max_regs(st, s, dst):
 
 def shift_block(st, b, sh, first):
     """m_ref moves by sh: S -= sh, m_ref += sh, negm = -m_ref; O, l *= 2^-sh"""
-    for ins in shift_ops([f"v{16 * b + i}" for i in range(16)], b, b, sh, first):
-        st.emit(ins)
-
-
-def shift_ops(sregs, ob, mb, sh, first):
-    """shift_block's instructions: scores sregs, accumulators O(ob) / L(ob),
-    m_ref MREF[mb] / NEGM(mb)"""
-    out = []
     if not first:
         alpha = T[3]
-        out.append(valu(f"v_exp_f32 {alpha}, -{sh}", r=[sh], w=[alpha], kind="trans"))
-        regs = [O(ob, e, i) for e in range(NE) for i in range(4)] + [L(ob, i) for i in range(4)]
+        st.emit(valu(f"v_exp_f32 {alpha}, -{sh}", r=[sh], w=[alpha], kind="trans"))
+        regs = [O(b, e, i) for e in range(NE) for i in range(4)] + [L(b, i) for i in range(4)]
         for a in regs:
-            out.append(valu(f"v_accvgpr_read_b32 {T[4]}, {a}", r=[a], w=[T[4]]))
-            out.append(valu(f"v_mul_f32 {T[4]}, {T[4]}, {alpha}", r=[T[4], alpha], w=[T[4]]))
-            out.append(valu(f"v_accvgpr_write_b32 {a}, {T[4]}", r=[T[4]], w=[a]))
-    for x in sregs:
-        out.append(valu(f"v_sub_f32 {x}, {x}, {sh}", r=[x, sh], w=[x]))
-    out.append(valu(f"v_add_f32 {MREF[mb]}, {MREF[mb]}, {sh}", r=[MREF[mb], sh], w=[MREF[mb]]))
+            st.emit(valu(f"v_accvgpr_read_b32 {T[4]}, {a}", r=[a], w=[T[4]]))
+            st.emit(valu(f"v_mul_f32 {T[4]}, {T[4]}, {alpha}", r=[T[4], alpha], w=[T[4]]))
+            st.emit(valu(f"v_accvgpr_write_b32 {a}, {T[4]}", r=[T[4]], w=[a]))
+    for i in range(16):
+        x = f"v{16 * b + i}"
+        st.emit(valu(f"v_sub_f32 {x}, {x}, {sh}", r=[x, sh], w=[x]))
+    st.emit(valu(f"v_add_f32 {MREF[b]}, {MREF[b]}, {sh}", r=[MREF[b], sh], w=[MREF[b]]))
     for i in range(4):
-        out.append(valu(f"v_xor_b32 {NEGM(mb, i)}, 0x80000000, {MREF[mb]}", r=[MREF[mb]], w=[NEGM(mb, i)]))
-    return out
+        st.emit(valu(f"v_xor_b32 {NEGM(b, i)}, 0x80000000, {MREF[b]}", r=[MREF[b]], w=[NEGM(b, i)]))
 
 
-def mask_block(st, b, causal, qr=None, kvh=None, sbase=None, ncb=4):
+def mask_block(st, b, causal):
     """S(b) = -inf where key >= kv_hi_b or (causal) key > query row, for the
     tile at key KV0 (key kv = KV0 + 16cb + 4sg + i, row = qr_b + r16):
     valid iff 16cb + i <= lim = min(kvh_b - KV0 - 1 - 4sg, qr_b - KV0 + r16 - 4sg).
-    A tile inside both bounds gets lim >= 63: a no-op.  (The split phase:
-    ncb = 2 key blocks at v[sbase ..], its own row base and bound.)"""
-    qr = QR[b] if qr is None else qr
-    kvh = KVH[b] if kvh is None else kvh
-    sbase = 16 * b if sbase is None else sbase
-    st.raw(f"s_sub_i32 {ST0}, {kvh}, {KV0}")
+    A tile inside both bounds gets lim >= 63: a no-op."""
+    st.raw(f"s_sub_i32 {ST0}, {KVH[b]}, {KV0}")
     st.raw(f"s_sub_i32 {ST0}, {ST0}, 1")
-    st.raw(f"s_sub_i32 {ST1}, {qr}, {KV0}")
+    st.raw(f"s_sub_i32 {ST1}, {QR[b]}, {KV0}")
     lim_rag, lim = T[5], T[7]
     st.emit(valu(f"v_sub_u32 {T[6]}, %[vt], %[r16]", r=["%[vt]", "%[r16]"], w=[T[6]]))   # -4sg
     st.emit(valu(f"v_add_u32 {lim_rag}, {ST0}, {T[6]}", r=[T[6]], w=[lim_rag]))
@@ -575,9 +546,9 @@ def mask_block(st, b, causal, qr=None, kvh=None, sbase=None, ncb=4):
         st.emit(valu(f"v_min_i32 {lim}, {lim}, {lim_rag}", r=[lim, lim_rag], w=[lim]))
     else:
         lim = lim_rag
-    for cb in range(ncb):
+    for cb in range(4):
         for i in range(4):
-            x = f"v{sbase + 4 * cb + i}"
+            x = S(b, cb, i)
             st.emit(valu(f"v_cmp_le_i32 vcc, {16 * cb + i}, {lim}", r=[lim]))
             st.emit(valu(f"v_cndmask_b32 {x}, {VNINF}, {x}, vcc", r=[VNINF, x], w=[x]))
 
@@ -601,346 +572,6 @@ def qk_plain(st, kb, nb):
         for b in range(nb):
             for m in qk_chain(b, cb):
                 st.emit(m)
-
-
-# ---------------------------------------------------------------------------
-# the split phase (W4_XP=split1, causal items whose blocks 2 and 3 are absent:
-# the pairs).  Once block 1 is done, block 0 alone would cost every wave the
-# whole K and V^T tile from LDS for 16 rows (LDS-bound: 4 x 32 KiB of reads per
-# tile).  With >= NS_MIN key tiles left, the waves switch layout: wave w =
-# (rh, kh) = (w >> 1, w & 1) takes rows 32 rh .. 32 rh + 31 of block 0 (two
-# 16-row blocks i, rows QR[2 + i] + r16, whose scaled Q the prologue loaded
-# into Q(2), Q(3)) against keys 32 kh .. 32 kh + 31 of every tile: half the
-# LDS reads for the same MFMAs.  Each wave keeps an independent partial
-# softmax per row block (O(2 + i), L(2 + i), MREF / NEGM / RMAX[2 + i], the
-# first tile centred on its own row max); at the end each wave merges, for
-# its own 16 rows, its old partial (O(0), keys before the switch), its own
-# split partial and its partner's (w ^ 1) through LDS.
-#   kind x (entry, iteration j): PV(j) of block 0 in the old layout, QK^T(j+1)
-#                                in the split one, the split's first softmax
-#   kind s (steady):             PV(j) / QK^T(j+1) split, lazy rescale
-#   kind sd (drain):             PV(j) split
-# ---------------------------------------------------------------------------
-SPLIT_XP = "split1" in w4.XP
-NS_MIN = int(os.environ.get("W4P_NSMIN", "3"))   # split tiles at least
-SNP_X, SNP_S, SNP_DONE = 5, 6, 7
-KAS = [R("v", 32 + t) for t in range(4)]   # K / V^T read addresses of the wave's key half
-VAS = [R("v", 36 + x) for x in range(2)]
-RS = [RMAX[2], RMAX[3]]
-
-
-def split_on(causal):
-    return SPLIT_XP and causal
-
-
-def ss_base(i, c=0):        # split scores: row block i, key block c (of the half): S(1, 2i + c)
-    return 16 + 8 * i + 4 * c
-
-
-def va_s():
-    return min(4, NE)
-
-
-def split_setup(st):
-    """the wave's key-half read addresses: + 32 kh rows"""
-    st.raw(f"s_and_b32 {STMP}, {QR[0]}, 16")
-    st.raw(f"s_lshl_b32 {STMP}, {STMP}, {ROWSH + 1}")
-    for t in range(NT):
-        st.emit(valu(f"v_add_u32 {KAS[t]}, {STMP}, {KADDR[t]}", r=[KADDR[t]], w=[KAS[t]]))
-    for x in range(2):
-        st.emit(valu(f"v_add_u32 {VAS[x]}, {STMP}, {VADDR[x]}", r=[VADDR[x]], w=[VAS[x]]))
-
-
-def k_read_s(t, c, kb):
-    s_ = kslot(c, t)
-    return dsr(f"ds_read_b128 {KF(s_)}, {KAS[t]} offset:{kb + 16 * ROWB * c}", KF(s_), KAS[t])
-
-
-def v_reads_s(e, vb):
-    off = vb + 512 * (e >> 1)
-    a = VAS[e & 1]
-    return [dsr(f"ds_read_b64_tr_b16 {VF(e, 0)}, {a} offset:{off}", VF(e, 0), a),
-            dsr(f"ds_read_b64_tr_b16 {VF(e, 1)}, {a} offset:{off + 16 * ROWB}", VF(e, 1), a)]
-
-
-def qk_chain_s(i, c):
-    out = []
-    sreg = R("v", ss_base(i, c), 4)
-    for t in range(NT):
-        cc = NEGM(2 + i) if t == 0 else sreg
-        out.append(mfma(sreg, KF(kslot(c, t)), Q(2 + i, t), cc))
-    return out
-
-
-def pv_mfmas_s():
-    ms, ff = [], {}
-    for e in range(NE):
-        ff[e] = len(ms)
-        for i in range(2):
-            ms.append(mfma(O(2 + i, e), VF(e), P(1, i), O(2 + i, e)))
-    ms += [mfma(L(2 + i), ONES, P(1, i), L(2 + i)) for i in range(2)]
-    return ms, ff
-
-
-def phase_a_split(st, p, mode):
-    """mode x: QK^T(j+1) split beside block 0's P(j) conversion (old layout)
-    and its first V^T reads; s: QK^T(j+1) split beside the split P(j)
-    conversions, maxima, V^T reads; sd: conversions and V^T reads alone.
-    The DMA as the one-block kind's."""
-    kb = KBUF[1 - p]
-    if mode == "sd":
-        for i in range(2):
-            for c in range(2):
-                for ins in cvt_block(1, 2 * i + c):
-                    st.emit(ins)
-        for e in range(va_s()):
-            for r in v_reads_s(e, VBUF[p]):
-                st.emit(r)
-        return [], []
-    chains = [(i, c) for c in range(2) for i in range(2)]
-    mf = []
-    for i, c in chains:
-        mf += qk_chain_s(i, c)
-    n = len(mf)
-    gaps = {}
-
-    def put(k, ins):
-        gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
-
-    if NT == 4:
-        put(0, [k_read_s(t, 0, kb) for t in range(NT)])
-        for t in range(NT):
-            put(1 + t % 3, k_read_s(t, 1, kb))
-    else:
-        put(0, [k_read_s(t, c, kb) for c in range(2) for t in range(NT)])
-    if mode == "s":
-        for x, (i, c) in enumerate(chains):
-            cv = cvt_block(1, 2 * i + c)
-            if x == 0:
-                put(0, cv)
-            else:
-                put(NT * x - 1, cv[0])
-                put(NT * x, cv[1])
-            if x >= lag():
-                iy, cy = chains[x - lag()]
-                mm = max_at(RS[iy], ss_base(iy, cy), first=(cy == 0))
-                put(min(NT * x + MAX_OFF, n), mm[0])
-                put(min(NT * x + MAX_OFF + 1, n), mm[1])
-    else:
-        extra = [cv for cb in range(4) for cv in cvt_block(0, cb)]
-        for k, cv in enumerate(extra):
-            put(1 + (k * (n - 2)) // len(extra), cv)
-    pairs, adv = dma_pieces(p)
-    late = []
-    if "p1dmaa" not in w4.XP:
-        late = [ins for pr in pairs[NPIECE:] for ins in pr] + [i for g in adv[2:] for i in g]
-        pairs, adv = pairs[:NPIECE], adv[:2]
-    for k, (m0, ld) in enumerate(pairs):
-        put(1 + k, m0)
-        put(2 + k, ld)
-    g = len(pairs) + 2
-    for k, ins in enumerate(adv):
-        put(min(g + k, n), ins)
-    if mode == "s":
-        va = va_s()
-        for e in range(va):
-            for k, r in enumerate(v_reads_s(e, VBUF[p])):
-                put(min(max(0, n - 2 * va) + 2 * e + k, n), r)
-    else:
-        va = vahead(1)
-        for f in range(va):
-            for k, r in enumerate(v_reads(f, VBUF[p])):
-                put(min(max(0, n - 2 * va) + 2 * f + k, n), r)
-    assert max(gaps) <= n
-    st.interleave(mf, gaps)
-    left = []
-    if mode == "s":
-        for y in range(max(0, len(chains) - lag()), len(chains)):
-            iy, cy = chains[y]
-            left += max_at(RS[iy], ss_base(iy, cy), first=(cy == 0))
-    return left, late
-
-
-def mask_pass_s(st, causal):
-    """tile j+1 is block 0's last: the limit mask of both split row blocks
-    (key base KV0 + 32 kh), then their maxima again"""
-    done = w4.newlabel("nomasks")
-    st.raw(f"s_cmp_eq_u32 {TB[0]}, {SJ2}")
-    st.branch("s_cbranch_scc0", done)
-    st.raw(f"s_lshl_b32 {KV0}, {SJ1}, 6")
-    st.raw(f"s_and_b32 {STMP}, {QR[0]}, 16")
-    st.raw(f"s_lshl_b32 {STMP}, {STMP}, 1")
-    st.raw(f"s_add_u32 {KV0}, {KV0}, {STMP}")
-    for i in range(2):
-        mask_block(st, 0, causal, qr=QR[2 + i], kvh=KVH[0], sbase=ss_base(i), ncb=2)
-        for c in range(2):
-            for ins in max_at(RS[i], ss_base(i, c), first=(c == 0)):
-                st.emit(ins)
-    st.label(done)
-
-
-def first_softmax_s_ops():
-    """the split's first tile: every row of each row block centres on its
-    max over the wave's key half (slow_softmax(first=True)'s arithmetic)"""
-    class Sink:
-        def __init__(self):
-            self.ops = []
-
-        def emit(self, ins):
-            self.ops.append(ins)
-    sk = Sink()
-    for i in range(2):
-        sregs = [f"v{ss_base(i) + k}" for k in range(8)]
-        mx, sh = T[1], T[2]
-        row_max_regs(sk, sregs, mx)
-        sk.emit(valu(f"v_cmp_eq_f32 vcc, {VNINF}, {mx}", r=[VNINF, mx]))
-        sk.emit(valu(f"v_cndmask_b32_e64 {sh}, {mx}, 0, vcc", r=[mx], w=[sh]))
-        sk.ops += shift_ops(sregs, 2 + i, 2 + i, sh, first=True)
-    return sk.ops
-
-
-def slow_softmax_s(st):
-    for i in range(2):
-        skip = w4.newlabel("pskips")
-        st.emit(valu(f"v_cmp_lt_f32 vcc, {RESCALE}, {RS[i]}", r=[RS[i]]))
-        st.branch("s_cbranch_vccz", skip)
-        sregs = [f"v{ss_base(i) + k}" for k in range(8)]
-        mx, sh = T[1], T[2]
-        row_max_regs(st, sregs, mx)
-        st.emit(valu(f"v_max_f32 {sh}, 0, {mx}", r=[mx], w=[sh]))
-        for ins in shift_ops(sregs, 2 + i, 2 + i, sh, first=False):
-            st.emit(ins)
-        st.label(skip)
-
-
-def phase_b_split(st, p, mode, leftover, label_slow, label_end, late):
-    vb = VBUF[p]
-    gaps = {}
-
-    def put(k, ins):
-        gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
-
-    for k, ins in enumerate(late):
-        put(1 + k, ins)
-    if mode == "x":
-        mf, ff = pv_mfmas(1)
-        va = vahead(1)
-        for f in range(va, 2 * NE):
-            r = v_reads(f, vb)
-            put(ff[f - va] + 1, r[0])
-            put(ff[f - va] + 2, r[1])
-        n = len(mf)
-        ops = first_softmax_s_ops() + exp_ops(1)
-        for k, ins in enumerate(ops):
-            put(1 + (k * (n - 1)) // len(ops), ins)
-        st.interleave(mf, gaps)
-        st.branch("s_branch", label_end)
-        return
-    mf, ff = pv_mfmas_s()
-    va = va_s()
-    for e in range(va, NE):
-        r = v_reads_s(e, vb)
-        put(ff[e - va] + 1, r[0])
-        put(ff[e - va] + 2, r[1])
-    if mode == "sd":
-        st.interleave(mf, gaps)
-        st.branch("s_branch", label_end)
-        return
-    lo = [LEFT_OFF + (i if NT == 4 else i // 2) for i in range(len(leftover))]
-    for k, ins in zip(lo, leftover):
-        put(k, ins)
-    assert not leftover or lo[-1] <= DEC_GAP
-    dec = [valu(f"v_max_f32 {T[0]}, {RS[0]}, {RS[1]}", r=RS, w=[T[0]]),
-           valu(f"v_cmp_lt_f32 vcc, {RESCALE}, {T[0]}", r=[T[0]])]
-    emit_b(st, mf, gaps, dec, exp_ops(1), lambda: slow_softmax_s(st), label_slow, label_end)
-
-
-def iteration_split(st, p, mode, causal, Lb):
-    stamp_path(st, NPATH - 1 if mode == "sd" else NB - 1)
-    if mode == "x":
-        split_setup(st)
-    left, late = phase_a_split(st, p, mode)
-    if mode == "s":
-        mask_pass_s(st, causal)
-    phase_b_split(st, p, mode, left, Lb["slow_s"][p], Lb["end"][p], late)
-
-
-def split_merge(st):
-    """after the loop (SNP = SNP_DONE): wave w hands its split partial of the
-    partner's row block (1 - kh) to LDS, takes the partner's of its own, and
-    merges them with its own split partial and its old one into O(0) / L(0)"""
-    reg = NE * 1024 + 512                       # bytes per wave: O^T (NE x 1 KiB) then m, l
-    base, wb, rb = "s40", "s41", "s42"
-    st.raw(f"s_and_b32 {ST0}, {QR[0]}, 48")      # 16 w
-    st.raw(f"s_lshl_b32 {base}, {ST0}, {ROWSH}")
-    st.raw(f"s_sub_u32 {base}, %[dmab], {base}")  # the images' base
-    st.raw(f"s_mul_i32 {wb}, {ST0}, {reg // 16}")
-    st.raw(f"s_add_u32 {wb}, {wb}, {base}")
-    st.raw(f"s_xor_b32 {rb}, {ST0}, 16")
-    st.raw(f"s_mul_i32 {rb}, {rb}, {reg // 16}")
-    st.raw(f"s_add_u32 {rb}, {rb}, {base}")
-    ln, aw, ar, mw, mr = "v40", "v41", "v42", "v43", "v44"
-    st.raw(f"v_mbcnt_lo_u32_b32 {ln}, -1, 0")
-    st.raw(f"v_mbcnt_hi_u32_b32 {ln}, -1, {ln}")
-    st.raw(f"v_lshlrev_b32 {aw}, 4, {ln}")
-    st.raw(f"v_lshlrev_b32 {mw}, 3, {ln}")
-    st.raw(f"v_add_u32 {ar}, {rb}, {aw}")
-    st.raw(f"v_add_u32 {aw}, {wb}, {aw}")
-    st.raw(f"v_add_u32 {mr}, {rb}, {mw}")
-    st.raw(f"v_add_u32 {mw}, {wb}, {mw}")
-    st.nop(2)
-    kh1, wdone = w4.newlabel("mkh1"), w4.newlabel("mwdone")
-    st.raw(f"s_and_b32 {STMP}, {QR[0]}, 16")
-    st.raw(f"s_cmp_eq_u32 {STMP}, 0")
-    st.branch("s_cbranch_scc0", kh1)
-    for kh in range(2):
-        if kh:
-            st.label(kh1)
-        i = 1 - kh                               # the partner's row block
-        for e in range(NE):
-            for k in range(4):
-                st.emit(valu(f"v_accvgpr_read_b32 v{4 * e + k}, {O(2 + i, e, k)}",
-                             r=[O(2 + i, e, k)], w=[f"v{4 * e + k}"]))
-        st.emit(valu(f"v_mov_b32 v48, {MREF[2 + i]}", r=[MREF[2 + i]], w=["v48"]))
-        st.emit(valu(f"v_accvgpr_read_b32 v49, {L(2 + i, 0)}", r=[L(2 + i, 0)], w=["v49"]))
-        st.nop(1)
-        for e in range(NE):
-            st.emit(w4.dsw(f"ds_write_b128 {aw}, v[{4 * e}:{4 * e + 3}] offset:{1024 * e}", aw,
-                           f"v[{4 * e}:{4 * e + 3}]"))
-        st.emit(w4.dsw(f"ds_write_b64 {mw}, v[48:49] offset:{NE * 1024}", mw, "v[48:49]"))
-        st.branch("s_branch", wdone)
-    st.label(wdone)
-    st.lgkm_all()
-    st.raw("s_barrier")
-    for e in range(NE):
-        st.emit(dsr(f"ds_read_b128 v[{4 * e}:{4 * e + 3}], {ar} offset:{1024 * e}",
-                    f"v[{4 * e}:{4 * e + 3}]", ar))
-    st.emit(dsr(f"ds_read_b64 v[48:49], {mr} offset:{NE * 1024}", "v[48:49]", mr))
-    st.lgkm_all()
-    kh1, mdone = w4.newlabel("mmkh1"), w4.newlabel("mmdone")
-    st.raw(f"s_cmp_eq_u32 {STMP}, 0")
-    st.branch("s_cbranch_scc0", kh1)
-    m, a0, a1, a2, t = T[0], T[1], T[2], T[3], T[4]
-    for kh in range(2):
-        if kh:
-            st.label(kh1)
-        ms = MREF[2 + kh]
-        st.emit(valu(f"v_max3_f32 {m}, {MREF[0]}, {ms}, v48", r=[MREF[0], ms, "v48"], w=[m]))
-        for dst, src in ((a0, MREF[0]), (a1, ms), (a2, "v48")):
-            st.emit(valu(f"v_sub_f32 {dst}, {src}, {m}", r=[src, m], w=[dst]))
-        for x in (a0, a1, a2):
-            st.emit(valu(f"v_exp_f32 {x}, {x}", r=[x], w=[x], kind="trans"))
-        regs = [(O(0, e, k), O(2 + kh, e, k), f"v{4 * e + k}") for e in range(NE) for k in range(4)]
-        regs.append((L(0, 0), L(2 + kh, 0), "v49"))
-        for o0, o1, o2 in regs:
-            st.emit(valu(f"v_accvgpr_read_b32 {t}, {o0}", r=[o0], w=[t]))
-            st.emit(valu(f"v_accvgpr_read_b32 {T[5]}, {o1}", r=[o1], w=[T[5]]))
-            st.emit(valu(f"v_mul_f32 {t}, {t}, {a0}", r=[t, a0], w=[t]))
-            st.emit(valu(f"v_fmac_f32_e32 {t}, {T[5]}, {a1}", r=[t, T[5], a1], w=[t]))
-            st.emit(valu(f"v_fmac_f32_e32 {t}, {o2}, {a2}", r=[t, o2, a2], w=[t]))
-            st.emit(valu(f"v_accvgpr_write_b32 {o0}, {t}", r=[t], w=[o0]))
-        st.branch("s_branch", mdone)
-    st.label(mdone)
 
 
 # iteration kinds (NP, NQ): steady, one block's drain, every block's drain
@@ -1181,10 +812,6 @@ def body(st, p, causal, Lb):
     st.raw(f"s_add_u32 {SJ1}, {SJ}, 1")
     st.raw(f"s_add_u32 {SJ2}, {SJ}, 2")
     lbl = {k: w4.newlabel(f"np{k}_") for k in range(1, NB + 1)}
-    if split_on(causal):
-        lsp = w4.newlabel("npsplit")
-        st.raw(f"s_cmp_gt_u32 {SNP}, {NB}")
-        st.branch("s_cbranch_scc1", lsp)
     for k in range(NB, 1, -1):
         st.raw(f"s_cmp_eq_u32 {SNP}, {k}")
         st.branch("s_cbranch_scc1", lbl[k])
@@ -1200,26 +827,7 @@ def body(st, p, causal, Lb):
     for np_, nq in KINDS:
         st.label(K(np_, nq))
         st.raw(f"s_mov_b32 {SNP}, {nq}")             # NP of iteration j+1
-        if split_on(causal) and (np_, nq) == (2, 1):
-            # block 1 ends here: the split phase follows when blocks 2, 3 are
-            # absent and block 0 has >= NS_MIN tiles after the entry kind's
-            st.raw(f"s_add_u32 {STMP}, {SJ}, {2 + NS_MIN}")
-            st.raw(f"s_cmp_eq_u32 {TB[2]}, 0")
-            st.raw(f"s_cselect_b32 {STMP}, {STMP}, 0x7fffffff")
-            st.raw(f"s_cmp_ge_u32 {TB[0]}, {STMP}")
-            st.raw(f"s_cselect_b32 {SNP}, {SNP_X}, 1")
         iteration(st, p, np_, nq, causal, Lb)
-    if split_on(causal):
-        st.label(lsp)
-        st.raw(f"s_cmp_eq_u32 {SNP}, {SNP_X}")
-        st.branch("s_cbranch_scc1", Lb["k_x"][p])
-        st.raw(f"s_cmp_gt_u32 {TB[0]}, {SJ1}")
-        st.branch("s_cbranch_scc1", Lb["k_s"][p])
-        st.branch("s_branch", Lb["k_sd"][p])
-        for mode, nxt in (("x", SNP_S), ("s", SNP_S), ("sd", SNP_DONE)):
-            st.label(Lb["k_" + mode][p])
-            st.raw(f"s_mov_b32 {SNP}, {nxt}")
-            iteration_split(st, p, mode, causal, Lb)
     st.label(Lb["end"][p], drain_lgkm=True)
     stamp_path_end(st)
     st.raw("s_waitcnt vmcnt(0)")   # this iteration's LDS-DMA landed before the barrier publishes it
@@ -1241,20 +849,11 @@ def generate(causal):
     Lb = {k: [w4.newlabel(f"{k}{p}") for p in range(2)]
           for k in ["loop", "end"] + [f"k_{kname(*x)}" for x in KINDS] + [f"slow_{kname(*x)}" for x in KINDS]}
     Lb["done"] = w4.newlabel("done")
-    if split_on(causal):
-        for k in ("k_x", "k_s", "k_sd", "slow_s"):
-            Lb[k] = [w4.newlabel(f"{k}{p}") for p in range(2)]
     prologue(st, causal)
     body(st, 0, causal, Lb)
     body(st, 1, causal, Lb)
     st.label(Lb["done"], drain_lgkm=True)
     stamp_now(st, 76)
-    if split_on(causal):
-        nomerge = w4.newlabel("nomerge")
-        st.raw(f"s_cmp_eq_u32 {SNP}, {SNP_DONE}")
-        st.branch("s_cbranch_scc0", nomerge)
-        split_merge(st)
-        st.label(nomerge)
     end = w4.newlabel("epidone")
     for b in range(NB):
         if b > 0:

@@ -84,5 +84,9 @@ res = {"shape": [a.batch, a.heads, a.seq], "causal": a.causal, "grouping": "quad
        "us_per_launch": round(us, 2), "mean": {n: round(float(m), 1) for n, m in zip(names, mean)},
        "per_iter": {n: round(float(mean[i] / max(mean[i + 5], 1e-9)), 1) for i, n in enumerate(names[:5])},
        "heaviest": {"rank": heavy[0], "wave": heavy[1], **{n: int(x) for n, x in zip(names, heavy[2])},
-                    "total": max(tot)}}
+                    "total": max(tot)},
+       "by_rank": {int(r): {n: round(float(np.mean([x[2][i] for x in rows if x[0] == r])), 1)
+                            for i, n in enumerate(names) if n in ("q2", "q1", "drain", "n_q2", "n_q1", "wait_bar",
+                                                                   "prologue", "epilogue")}
+                   for r in sorted({x[0] for x in rows})}}
 print(json.dumps(res))
