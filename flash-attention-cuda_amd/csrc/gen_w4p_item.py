@@ -265,16 +265,6 @@ def exp_ops(b):
             for x in range(16 * b, 16 * b + 16)]
 
 
-def pv_mfmas_x():
-    """pv_mfmas(1) on the one-block kind's fragment slots"""
-    ms = []
-    for u in range(2):
-        for e in range(NE):
-            ms.append(mfma(O(0, e), VX(u * NE + e), P(0, u), O(0, e)))
-        ms.append(mfma(L(0), ONES, P(0, u), L(0)))
-    return ms
-
-
 def pv_mfmas(np_):
     """PV + row sums of blocks 0..np-1: for u: for e: the blocks; then their row sums"""
     ms, frag_first = [], {}
@@ -285,39 +275,6 @@ def pv_mfmas(np_):
                 ms.append(mfma(O(b, e), VF((u * NE + e) % 8), P(b, u), O(b, e)))
         ms += [mfma(L(b), ONES, P(b, u), L(b)) for b in range(np_)]
     return ms, frag_first
-
-
-AHEAD_XP = "p1ahead" in w4.XP
-# the one-block kind's extra fragment slots (blocks 1-3's free S / P registers)
-VXB = [144 + 4 * i for i in range(8)] + [48, 52, 56, 60, 80, 84, 88, 92]
-
-
-def one_ahead(nq, np_):
-    """head_dim 128, one live block: every K fragment of the tile and every
-    V^T fragment of PV(j) read in phase A (16 + 16 slots), so no read feeds
-    its single MFMA with less than a chain of cover"""
-    return AHEAD_XP and nq == 1 and np_ == 1 and NT == 4
-
-
-def KX(slot):
-    return KF(slot) if slot < 8 else R("v", 16 + 4 * (slot - 8), 4)
-
-
-def VX(slot, half=None):
-    base = VXB[slot]
-    return R("v", base, 4) if half is None else R("v", base + 2 * half, 2)
-
-
-def k_read_x(t, cb, kb):
-    return dsr(f"ds_read_b128 {KX(4 * cb + t)}, {KADDR[t]} offset:{kb + 16 * ROWB * cb}", KX(4 * cb + t), KADDR[t])
-
-
-def v_reads_x(f, vb):
-    u, e = divmod(f, NE)
-    off = vb + 32 * ROWB * u + 512 * (e >> 1)
-    a = VADDR[e & 1]
-    return [dsr(f"ds_read_b64_tr_b16 {VX(f, 0)}, {a} offset:{off}", VX(f, 0), a),
-            dsr(f"ds_read_b64_tr_b16 {VX(f, 1)}, {a} offset:{off + 16 * ROWB}", VX(f, 1), a)]
 
 
 def dma_pieces(p):
@@ -359,24 +316,16 @@ def phase_a(st, p, nq, np_):
                 st.emit(r)
         return [], []
     chains = [(b, cb) for cb in range(4) for b in range(nq)]
-    ahead = one_ahead(nq, np_)
     mf = []
     for b, cb in chains:
-        if ahead:
-            mf += [mfma(S(b, cb), KX(4 * cb + t), Q(b, t), NEGM(b) if t == 0 else S(b, cb)) for t in range(NT)]
-        else:
-            mf += qk_chain(b, cb)
+        mf += qk_chain(b, cb)
     n = len(mf)
     gaps = {}
 
     def put(k, ins):
         gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
 
-    if ahead:
-        for cb in range(4):
-            put(cb, [k_read_x(t, cb, kb) for t in range(NT)])
-    else:
-        put(0, [k_read(t, 0, kb) for t in range(NT)] if NT == 4 else k_reads_tile(kb))
+    put(0, [k_read(t, 0, kb) for t in range(NT)] if NT == 4 else k_reads_tile(kb))
     for x, (b, cb) in enumerate(chains):
         c = cvt_block(b, cb)
         if cb == 0:
@@ -384,7 +333,7 @@ def phase_a(st, p, nq, np_):
         else:
             put(NT * x - 1, c[0])
             put(NT * x, c[1])
-        if b == 0 and cb < 3 and NT == 4 and not ahead:
+        if b == 0 and cb < 3 and NT == 4:
             for t in range(NT):
                 put(NT * x + 1 + t % 3, k_read(t, cb + 1, kb))
         if x >= lag():
@@ -416,14 +365,9 @@ def phase_a(st, p, nq, np_):
     for i, ins in enumerate(adv):
         put(min(g + i, n), ins)
     # the first V^T fragments of PV(j) (V(j) is ready since the last barrier)
-    if ahead:
-        for f in range(2 * NE):
-            for i, r in enumerate(v_reads_x(f, VBUF[p])):
-                put(4 + ((2 * f + i) * (n - 4)) // (4 * NE), r)
-    else:
-        for f in range(va):
-            for i, r in enumerate(v_reads(f, VBUF[p])):
-                put(min(max(0, n - 2 * va) + 2 * f + i, n), r)
+    for f in range(va):
+        for i, r in enumerate(v_reads(f, VBUF[p])):
+            put(min(max(0, n - 2 * va) + 2 * f + i, n), r)
     assert max(gaps) <= n, "every filler lands in a gap"
     st.interleave(mf, gaps)
     left = []
@@ -462,8 +406,6 @@ def phase_b(st, p, nq, np_, leftover, label_slow, label_end, late=()):
     PV alone."""
     vb = VBUF[p]
     mf, frag_first = pv_mfmas(np_)
-    if one_ahead(nq, np_):
-        mf = pv_mfmas_x()
     n = len(mf)
     gaps = {}
 
@@ -473,7 +415,7 @@ def phase_b(st, p, nq, np_, leftover, label_slow, label_end, late=()):
     # phase A's deferred DMA: (M0, load) pairs an MFMA apart, then the advance
     for i, ins in enumerate(late):
         put(1 + i, ins)
-    va = 2 * NE if one_ahead(nq, np_) else vahead(np_)
+    va = vahead(np_)
     for f in range(va, 2 * NE):
         k = frag_first[f - va]
         r = v_reads(f, vb)
