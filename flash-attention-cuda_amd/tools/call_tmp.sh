@@ -1,8 +1,6 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-AB="timeout -k 10 300 python flash-attention-cuda_amd/tools/ab.py --configs auto --libs ,p1noexp,p1nobar --rounds 9 --iters 40"
-O=gpurun_out/r05_ab_w4p_probes2.jsonl
-$AB --seq 1024 --causal > $O &&
-$AB --seq 4096 --heads 8 --causal >> $O || exit 1
-cat $O
+timeout -k 10 600 python -u -m pytest tests/test_dispatch_sweep_gpu.py -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/r05_pytest_dispatch_sweep.log 2>&1; rc=$?
+tail -15 gpurun_out/r05_pytest_dispatch_sweep.log
+exit $rc

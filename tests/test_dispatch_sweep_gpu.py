@@ -1,0 +1,114 @@
+"""Dispatcher-level sweep: random and tier-boundary shapes through both entry
+points a caller has -- the Python/torch path (`flash_attention_fwd`, which
+brings the workspace: causal split tier, W4 tail pool) and the
+workspace-free C entry (`fa_fwd_f16` / `fa_fwd_bf16`, what the reference's
+`flash_attention_v9_dispatch` signature reaches, flash_attention.cu:606-611)
+-- against an fp32 torch attention of the same 16-bit inputs.
+
+The per-tier tests force one config each; this file checks that the
+dispatcher's choice (`fa_select_config`, the split / pool / W4P / W4 /
+KV-pair / KV-quad / loop boundaries in fa_fwd.hip) is right wherever it
+lands: every shape must match at 1e-3 (fp16) or 5e-3 (bf16), whichever tier
+runs it.
+"""
+import math
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+def _fa():
+    import fa_mi355x
+
+    return fa_mi355x
+
+
+def _random_shapes(n, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < n:
+        b = int(rng.integers(1, 5))
+        h = int(rng.integers(1, 41))
+        s = int(round(math.exp(rng.uniform(0.0, math.log(5000)))))
+        d = int(rng.choice([64, 128]))
+        causal = bool(rng.integers(0, 2))
+        bf16 = bool(rng.random() < 0.3)
+        while b * h * s * s * d > 4e9 and s > 1:
+            s //= 2
+        out.append((b, h, s, d, causal, bf16))
+    return out
+
+
+# tier boundaries of the dispatcher (fa_fwd.hip select_tier / launch_auto):
+# config 1 and its ragged neighbours (W4P pairs), few-head long causal (W4P
+# pairs vs the workspace split tier), two rounds of pairs (quads), W4
+# persistent from two rounds of 256-row items, the S <= 256 loop, the KV-quad
+# under-filled non-causal case, the tail-pool shape class (>= 64 rounds per
+# XCD, a reduced copy), d64 twins
+BOUNDARY = [
+    (1, 32, 1024, 128, True, False), (1, 32, 1023, 128, True, False), (1, 32, 1025, 128, True, False),
+    (1, 32, 1024, 128, False, False), (1, 8, 4096, 128, True, False), (1, 4, 8192, 128, True, False),
+    (2, 32, 1024, 128, True, False), (1, 16, 4096, 128, True, False), (4, 32, 1024, 128, True, False),
+    (1, 32, 256, 128, True, False), (1, 32, 257, 128, False, False), (1, 32, 512, 128, False, False),
+    (1, 32, 512, 128, True, False), (3, 5, 77, 128, True, False), (1, 1, 1, 128, False, False),
+    (1, 32, 1024, 64, True, False), (1, 8, 4096, 64, True, False), (2, 16, 2048, 64, False, False),
+    (1, 32, 1024, 128, True, True), (1, 4, 8192, 128, True, True), (1, 32, 2048, 64, True, True),
+]
+
+
+def _ref(q, k, v, causal):
+    b, h, s, d = q.shape
+    out = torch.empty((b, h, s, d), dtype=torch.float32, device=q.device)
+    mask = torch.ones((s, s), dtype=torch.bool, device=q.device).tril() if causal else None
+    for bi in range(b):
+        for hi in range(h):
+            sc = (q[bi, hi].float() @ k[bi, hi].float().t()) / math.sqrt(d)
+            if causal:
+                sc = sc.masked_fill(~mask, float("-inf"))
+            out[bi, hi] = torch.softmax(sc, dim=-1) @ v[bi, hi].float()
+    return out
+
+
+def _inputs(b, h, s, d, dtype, seed):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    return [torch.empty((b, h, s, d), dtype=torch.float32, device="cuda").uniform_(-0.5, 0.5, generator=g)
+            .to(dtype) for _ in range(3)]
+
+
+def _run(shape, seed):
+    fa = _fa()
+    b, h, s, d, causal, bf16 = shape
+    dtype = torch.bfloat16 if bf16 else torch.float16
+    tol = 5e-3 if bf16 else 1e-3
+    q, k, v = _inputs(b, h, s, d, dtype, seed)
+    ref = _ref(q, k, v, causal)
+    # the Python / torch path: workspace entry
+    o1 = fa.flash_attention_fwd(q, k, v, causal)
+    torch.cuda.synchronize()
+    err1 = (o1.float() - ref).abs().max().item()
+    # the workspace-free C entry (the reference signature's path)
+    o2 = torch.full_like(q, float("nan"))
+    lib = fa.load_library()
+    fn = lib.fa_fwd_bf16 if bf16 else lib.fa_fwd_f16
+    rc = fn(q.data_ptr(), k.data_ptr(), v.data_ptr(), o2.data_ptr(), b, h, s, d, int(causal),
+            torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, lib.fa_status_string(rc)
+    torch.cuda.synchronize()
+    err2 = (o2.float() - ref).abs().max().item()
+    cfg = fa.configs()[fa.select_config(b, h, s, causal)].name if d == 128 and not bf16 else "-"
+    assert err1 <= tol and err2 <= tol, (shape, cfg, err1, err2)
+
+
+@pytest.mark.parametrize("shape", _random_shapes(40, 2028), ids=lambda s: "x".join(map(str, s)))
+def test_dispatch_random(shape):
+    _run(shape, 11)
+
+
+@pytest.mark.parametrize("shape", BOUNDARY, ids=lambda s: "x".join(map(str, s)))
+def test_dispatch_boundary(shape):
+    _run(shape, 23)
