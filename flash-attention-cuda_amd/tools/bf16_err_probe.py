@@ -7,7 +7,7 @@ scales 1, 4 and 6, prints the max-abs error against the fp32 model of
   qc_rounding_alone   the fp32 model with Q * scale * log2(e) rounded to bf16
                       (the product every bf16 tier feeds its QK^T MFMA)
   ours_vs_qc_model    the kernel against that rounded model
-usage: python tools/bf16_err_probe.py   (on a GPU box)
+usage: python tools/bf16_err_probe.py [VARIANT]   (on a GPU box)
 """
 import json
 import math
@@ -22,6 +22,9 @@ import torch  # noqa: E402
 import test_dispatch_sweep_gpu as t  # noqa: E402
 
 fa = t._fa()
+if len(sys.argv) > 1:  # a variant library: tools/w4_variant.sh NAME ...
+    fa.LIB_PATH = os.path.join(os.path.dirname(fa.LIB_PATH), f"libfa_mi355x_{sys.argv[1]}.so")
+    fa._lib = None
 for shape in [s for s in t.BOUNDARY if s[5]]:
     b, h, s, d, causal, _ = shape
     for scale in (1.0, 4.0, 6.0):
