@@ -1,9 +1,6 @@
-# Scratch GPU call script (gpurun -- 'bash flash-attention-cuda_amd/tools/call_tmp.sh').
-# Left at the round's final-tree pass: parity + smoke + bench + rocprof +
-# harness (tools/gpu_check.sh), then the SDPA head-to-heads.
+# Scratch GPU call script: the driver's torchrun launch mode at N=1 on the final tree.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-ROUND=r05 bash flash-attention-cuda_amd/tools/gpu_check.sh || exit 1
-bash flash-attention-cuda_amd/tools/vs_sdpa_all.sh || exit 1
-echo done
+timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 20 --warmup 5 --no-sweep --no-cpu-baseline > gpurun_out/r05_bench_torchrun_n1.json 2> gpurun_out/r05_bench_torchrun_n1.err || { tail -20 gpurun_out/r05_bench_torchrun_n1.err; exit 1; }
+cat gpurun_out/r05_bench_torchrun_n1.json
