@@ -531,7 +531,8 @@ static int check_args(const void* q, const void* k, const void* v, const void* o
 }
 
 // W4 launches with a cross-XCD tail pool (fa_w4_kernel.hpp): the snake order
-// (not the causal pairs of <= 64 heads) with >= 16 rounds per XCD list
+// (not the causal pairs of <= 64 heads) with >= 64 rounds per XCD list
+// (w4_pool_rounds)
 static bool w4_pool_on(const Config& cfg, long long bh, int nqb, long long blocks) {
   if (cfg.kind != 5 || blocks < 8) return false;
   if (cfg.info.causal && bh <= 64 && bh % 8 == 0 && nqb % 2 == 0) return false;  // pairs
@@ -727,17 +728,20 @@ static int select_tier(int batch, int heads, int seq_len, int causal, bool pair)
 }
 
 namespace fa {
+// the paired tier (W4P) at head_dim 64 only for causal launches: non-causal
+// its d64 twin trails the KV-pair / W4 d64 (B=1 H=4 S=8192 851 vs 886, H=16
+// S=2048 722 vs 744); causal it leads (H=32 S=1024 374 vs 301, S=2048 quad
+// 653 vs 582, B=2 S=1024 502 vs 410; profiles/r05_ab_w4p_d64.jsonl).  One
+// rule for the launch and for fa_fwd_ws_bytes / the pool decision.
+static bool pair_tier_ok(int head_dim, int causal) { return head_dim == HD || causal; }
+
 static int launch_auto(int dtype, const void* q, const void* k, const void* v, void* o,
                            int batch, int heads, int seq_len, int head_dim, int causal,
                            void* hip_stream, unsigned* pool_ctr) {
   int rc = check_args(q, k, v, o, batch, heads, seq_len, head_dim);
   if (rc != FA_OK) return rc;
   if (batch == 0 || heads == 0 || seq_len == 0) return FA_OK;
-  // the paired tier at head_dim 64 only for causal launches: non-causal its
-  // d64 twin trails the KV-pair / W4 d64 (B=1 H=4 S=8192 851 vs 886, H=16
-  // S=2048 722 vs 744); causal it leads (H=32 S=1024 374 vs 301, S=2048 quad
-  // 653 vs 582, B=2 S=1024 502 vs 410; profiles/r05_ab_w4p_d64.jsonl)
-  const int sel = select_tier(batch, heads, seq_len, causal, head_dim == HD || causal);
+  const int sel = select_tier(batch, heads, seq_len, causal, pair_tier_ok(head_dim, causal));
   // (head_dim 64 of the W4 tier is the same item program with 2-step QK^T
   // chains and 8-KiB packed tiles: +4-9 % over the 8-wave ping-pong at
   // head_dim 64, profiles/r04_ab_w4_d64.jsonl, r05_ab_d64dma.jsonl)
@@ -751,7 +755,8 @@ static int launch_auto(int dtype, const void* q, const void* k, const void* v, v
 // tail pool (its counters live in the workspace's counter region)
 static bool auto_pool(int batch, int heads, int seq_len, int head_dim, int causal) {
   if (batch <= 0 || heads <= 0 || seq_len <= 0 || (head_dim != HD && head_dim != 64)) return false;
-  const int id = twin(select_tier(batch, heads, seq_len, causal, head_dim == HD), FA_DTYPE_F16, head_dim);
+  const int id = twin(select_tier(batch, heads, seq_len, causal, pair_tier_ok(head_dim, causal)),
+                      FA_DTYPE_F16, head_dim);
   if (id < 0 || kConfigs[id].kind != 5) return false;
   const long long bh = (long long)batch * heads;
   const int nqb = (seq_len + kConfigs[id].info.block_m - 1) / kConfigs[id].info.block_m;
@@ -911,11 +916,15 @@ static int launch_ws(int dtype, const void* q, const void* k, const void* v, voi
   if (sp.T == 0) {
     // the W4 tier's tail pool when the workspace holds its counters (else
     // the static order: a workspace is optional there)
-    const bool pool = ws && ws_bytes >= kSplitCtrBytes && auto_pool(batch, heads, seq_len, head_dim, causal);
+    // (its 64-bit claim counters need an 8-byte aligned workspace: a
+    // misaligned one runs the static order, as no workspace does)
+    const bool pool = ws && ws_bytes >= kSplitCtrBytes && (reinterpret_cast<uintptr_t>(ws) & 7) == 0 &&
+                      auto_pool(batch, heads, seq_len, head_dim, causal);
     return launch_auto(dtype, q, k, v, o, batch, heads, seq_len, head_dim, causal, hip_stream,
                        pool ? static_cast<unsigned*>(ws) : nullptr);
   }
-  if (!ws || ws_bytes < sp.bytes()) return FA_ERR_WORKSPACE;
+  // the slabs take 16-B sc1 stores / loads: a 16-byte aligned workspace
+  if (!ws || ws_bytes < sp.bytes() || (reinterpret_cast<uintptr_t>(ws) & 15) != 0) return FA_ERR_WORKSPACE;
   const int bh = batch * heads;
   return dtype == FA_DTYPE_BF16
              ? launch_split<true>(sp, q, k, v, o, bh, seq_len, ws, (hipStream_t)hip_stream)

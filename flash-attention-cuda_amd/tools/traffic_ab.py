@@ -35,7 +35,7 @@ def child(a):
                for _ in range(3))
     o = torch.empty_like(q)
     for _ in range(a.iters):
-        fa.flash_attention_fwd(q, k, v, a.causal, out=o, config=a.config)
+        fa.flash_attention_fwd(q, k, v, a.causal, out=o, config=None if a.config == "auto" else int(a.config))
     torch.cuda.synchronize()
 
 
@@ -54,7 +54,8 @@ def counter(root, name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--libs", default="")
-    ap.add_argument("--config", type=int, required=True)
+    ap.add_argument("--config", required=True, help="tile config id, or auto (the default dispatch: "
+                    "workspace path, tail pool)")
     ap.add_argument("--shapes", required=True, help="BxHxS[,BxHxS...]")
     ap.add_argument("--causal", action="store_true")
     ap.add_argument("--iters", type=int, default=3)
@@ -74,7 +75,7 @@ def main():
                 with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
                     cmd = ["timeout", "-s", "KILL", "120", prof, "--pmc", ctr, "-d", td, "--output-format",
                            "csv", "--", sys.executable, os.path.abspath(__file__), "--child", "--lib", lib,
-                           "--config", str(a.config), "--shapes", shape, "--iters", str(a.iters)]
+                           "--config", a.config, "--shapes", shape, "--iters", str(a.iters)]
                     if a.causal:
                         cmd.append("--causal")
                     r = subprocess.run(cmd, capture_output=True, text=True)

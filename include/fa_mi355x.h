@@ -135,9 +135,16 @@ unsigned long long fa_splitkv_ml_bytes(int batch, int heads, int seq_len,
  * (counters, the same place for every shape) must be zero before the first
  * use; every launch returns the counters it used to zero, so one buffer of
  * the largest size needed serves any sequence of shapes on ONE stream
- * (launches on different streams need their own).  FA_ERR_WORKSPACE if the
- * call splits and workspace is NULL or ws_bytes is short; a tail-pool shape
- * with no (or a short) workspace runs the static item order. */
+ * (launches on different streams need their own).  A counter region that is
+ * not zero (a fresh buffer never cleared, or one shared by two streams at
+ * once) is not detected: pool items can be skipped and their rows left
+ * unwritten, and the split merge can run early.  The workspace must be
+ * 16-byte aligned (any hipMalloc / torch allocation is): FA_ERR_WORKSPACE if
+ * the call splits and workspace is NULL, misaligned or ws_bytes is short; a
+ * tail-pool shape with no, a short or a misaligned (not 8-byte) workspace
+ * runs the static item order.  The reference-signature wrapper
+ * flash_attention_v9_dispatch (flash_attention_v9.h) owns such a workspace
+ * per (device, stream), so it runs the same tiers as these entries. */
 unsigned long long fa_fwd_ws_bytes(int batch, int heads, int seq_len, int head_dim,
                                    int causal, int piece_tiles);
 int fa_fwd_split_pieces(int batch, int heads, int seq_len, int head_dim, int causal);
@@ -167,7 +174,8 @@ int fa_fwd_bf16_ws(const void* q, const void* k, const void* v, void* o,
  * fa_config_info): they are not stable across releases (round 3 renumbered
  * 0-49 to 0-43 when the table was trimmed to the dispatched tiers; round 4
  * appended the head_dim-64 W4 configs 44-47; round 5 the paired
- * short-sequence configs 48-51 and their four-block twins 52-55).  Select a tier by its
+ * short-sequence configs 48-51, their four-block twins 52-55 and the
+ * head_dim-64 twins of both, 56-63).  Select a tier by its
  * fa_config_info().name, not by a remembered id. */
 int fa_select_config(int batch, int heads, int seq_len, int causal);
 

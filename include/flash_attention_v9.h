@@ -16,6 +16,12 @@
  * (its dispatcher never launches the split-K path; callers pass nullptr,
  * :777).  Split-KV is the explicit C entry fa_fwd_f16_splitkv (fa_mi355x.h),
  * which takes the split count and the buffers explicitly.
+ * Tiers: the same as the workspace entries (fa_fwd_f16_ws): the wrapper keeps
+ * one zero-filled device workspace per (device, stream) for the causal split
+ * tier and the W4 tail pool, allocated on the first call that needs one and
+ * grown outside graph capture only (a call captured before it exists runs
+ * the workspace-free tiers of fa_fwd_f16).  The reference allocates nothing
+ * here; this is the one host-side state besides the kernels' LDS attribute.
  */
 #ifndef FLASH_ATTENTION_V9_H
 #define FLASH_ATTENTION_V9_H

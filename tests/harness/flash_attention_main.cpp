@@ -83,26 +83,46 @@ static void register_report() {
   printf("\n");
 }
 
-static void bench_one(int seq, int heads, bool causal) {
-  const int batch = 1, hd = 128, runs_n = 3;
-  const size_t n = (size_t)batch * heads * seq * hd, sz = n * sizeof(uint16_t);
-  int cid = fa_select_config(batch, heads, seq, causal ? 1 : 0);
+// the tier flash_attention_v9_dispatch runs for a shape (it owns a workspace,
+// so it takes the split tier / the W4 tail pool where the dispatcher does)
+static const char* tier_label(int batch, int heads, int seq, bool causal, char* buf, size_t n) {
+  const int c = causal ? 1 : 0;
+  const int T = fa_fwd_split_pieces(batch, heads, seq, 128, c);
+  if (T > 0) {
+    snprintf(buf, n, "causal_split_T%d", T);
+    return buf;
+  }
   fa_config_info_t ci;
-  fa_config_info(cid, &ci);
+  fa_config_info(fa_select_config(batch, heads, seq, c), &ci);
+  const bool pool = fa_fwd_ws_bytes(batch, heads, seq, 128, c, 0) > 0;
+  snprintf(buf, n, "%s%s", ci.name, pool ? "+pool" : "");
+  return buf;
+}
+
+static void bench_one(int seq, int heads, bool causal, int batch = 1) {
+  const int hd = 128, runs_n = 3;
+  const size_t n = (size_t)batch * heads * seq * hd, sz = n * sizeof(uint16_t);
+  char label[128];
+  const char* name = tier_label(batch, heads, seq, causal, label, sizeof(label));
   if (sz * 4 > 15ULL * 1024 * 1024 * 1024) {  // :918-921
-    printf("%-6d  %-5d  %-28s  SKIP\n", seq, heads, ci.name);
+    printf("%-3d %-6d  %-5d  %-28s  SKIP\n", batch, seq, heads, name);
     return;
   }
-  std::vector<uint16_t> q(n), k(n), v(n);
-  fa_oracle_gen_inputs(q.data(), k.data(), v.data(), n, 42);
+  // the reference's srand(42) inputs for one batch entry (:924-929), copied to
+  // every batch entry (the generator would take minutes at B = 64)
+  const size_t n1 = (size_t)heads * seq * hd, sz1 = n1 * sizeof(uint16_t);
+  std::vector<uint16_t> q(n1), k(n1), v(n1);
+  fa_oracle_gen_inputs(q.data(), k.data(), v.data(), n1, 42);
   half *dq, *dk, *dv, *dout;
   HIP_CHECK(hipMalloc(&dq, sz));
   HIP_CHECK(hipMalloc(&dk, sz));
   HIP_CHECK(hipMalloc(&dv, sz));
   HIP_CHECK(hipMalloc(&dout, sz));
-  HIP_CHECK(hipMemcpy(dq, q.data(), sz, hipMemcpyHostToDevice));
-  HIP_CHECK(hipMemcpy(dk, k.data(), sz, hipMemcpyHostToDevice));
-  HIP_CHECK(hipMemcpy(dv, v.data(), sz, hipMemcpyHostToDevice));
+  for (int b = 0; b < batch; ++b) {
+    HIP_CHECK(hipMemcpy(dq + b * n1, q.data(), sz1, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dk + b * n1, k.data(), sz1, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dv + b * n1, v.data(), sz1, hipMemcpyHostToDevice));
+  }
   double flops = 4.0 * batch * heads * (double)seq * seq * hd;
   if (causal) flops /= 2;
   float runs[runs_n], sum = 0;
@@ -134,8 +154,8 @@ static void bench_one(int seq, int heads, bool causal) {
   }
   const float avg = sum / runs_n;
   const double peak = 256 * 2.4e9 * 4096 / 1e12;
-  printf("%-6d  %-5d  %-28s  %7.1f  %7.1f  %7.1f  %7.1f  (%4.1f%% MFMA peak)\n", seq, heads,
-         ci.name, runs[0], runs[1], runs[2], avg, 100.0 * avg / peak);
+  printf("%-3d %-6d  %-5d  %-28s  %7.1f  %7.1f  %7.1f  %7.1f  (%4.1f%% MFMA peak)\n", batch, seq,
+         heads, name, runs[0], runs[1], runs[2], avg, 100.0 * avg / peak);
   HIP_CHECK(hipFree(dq));
   HIP_CHECK(hipFree(dk));
   HIP_CHECK(hipFree(dv));
@@ -165,8 +185,8 @@ int main(int argc, char** argv) {
   if (argc > 1) {  // README.md:83-85 CLI: seq [causal]
     const int seq = atoi(argv[1]);
     const bool c = argc > 2 ? atoi(argv[2]) != 0 : true;
-    printf("%-6s  %-5s  %-28s  Run1     Run2     Run3     Avg (TFLOPS)\n", "seq", "heads",
-           "config");
+    printf("%-3s %-6s  %-5s  %-28s  Run1     Run2     Run3     Avg (TFLOPS)\n", "B", "seq",
+           "heads", "tier");
     bench_one(seq, 32, c);
     return all_ok ? 0 : 1;
   }
@@ -179,10 +199,19 @@ int main(int argc, char** argv) {
       sleep(cooldown);
     }
     printf("\n=== %s ===\n", bc ? "CAUSAL" : "NON-CAUSAL");
-    printf("%-6s  %-5s  %-28s  Run1     Run2     Run3     Avg (TFLOPS)\n", "seq", "heads",
-           "config");
+    printf("%-3s %-6s  %-5s  %-28s  Run1     Run2     Run3     Avg (TFLOPS)\n", "B", "seq",
+           "heads", "tier");
     printf("-----------------------------------------------------------------------------\n");
     for (int s : seqs) bench_one(s, 32, bc);
   }
+  // beyond the reference: the shapes whose tier needs the wrapper's workspace
+  // -- BASELINE config 5 on one GPU (the W4 tail pool) and long few-head
+  // causal launches (the causal split tier)
+  printf("\n=== WORKSPACE TIERS (causal) ===\n");
+  printf("%-3s %-6s  %-5s  %-28s  Run1     Run2     Run3     Avg (TFLOPS)\n", "B", "seq", "heads",
+         "tier");
+  bench_one(4096, 32, true, 64);
+  bench_one(8192, 4, true);
+  bench_one(16384, 2, true);
   return all_ok ? 0 : 1;
 }

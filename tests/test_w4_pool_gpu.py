@@ -127,3 +127,36 @@ def test_pool_without_counters_is_static():
     assert lib.fa_fwd_f16_ws(p(q), p(k), p(v), p(o), b, h, s, 128, 1, 0, None, 0, st) == fa.FA_OK
     torch.cuda.synchronize()
     assert torch.equal(o, _static(q, k, v, True))
+
+
+def test_pool_misaligned_workspace_is_static():
+    """the 64-bit claim counters need an 8-byte aligned workspace: a misaligned
+    one (here 4 bytes in, holding garbage that would make a pool skip items)
+    runs the static order and is never touched; the split tier rejects a
+    workspace that is not 16-byte aligned (advice r05)"""
+    fa = _fa()
+    lib = fa.load_library()
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    b, h, s = 32, 32, 4096
+    q, k, v = (_rand((b, h, s, 128), 980 + i) for i in range(3))
+    o = torch.empty_like(q)
+    ws = torch.full((CTR + 64,), 0xFF, dtype=torch.uint8, device="cuda")
+    mis = ctypes.c_void_p(ws.data_ptr() + 4)
+    assert lib.fa_fwd_f16_ws(p(q), p(k), p(v), p(o), b, h, s, 128, 1, 0, mis, CTR, st) == fa.FA_OK
+    torch.cuda.synchronize()
+    assert torch.equal(o, _static(q, k, v, True))
+    assert bool((ws == 0xFF).all())
+    # a split shape (B=1 H=4 S=8192 causal) with an 8-byte (not 16) aligned workspace
+    b, h, s = 1, 4, 8192
+    need = lib.fa_fwd_ws_bytes(b, h, s, 128, 1, 0)
+    assert need > CTR and lib.fa_fwd_split_pieces(b, h, s, 128, 1) > 0
+    q, k, v = (_rand((b, h, s, 128), 990 + i) for i in range(3))
+    o = torch.empty_like(q)
+    ws = torch.zeros(need + 64, dtype=torch.uint8, device="cuda")
+    assert lib.fa_fwd_f16_ws(p(q), p(k), p(v), p(o), b, h, s, 128, 1, 0, ctypes.c_void_p(ws.data_ptr() + 8),
+                             need, st) == fa.FA_ERR_WORKSPACE
+    assert lib.fa_fwd_f16_ws(p(q), p(k), p(v), p(o), b, h, s, 128, 1, 0, ctypes.c_void_p(ws.data_ptr() + 16),
+                             need, st) == fa.FA_OK
+    torch.cuda.synchronize()
+    assert torch.equal(o, fa.flash_attention_fwd(q, k, v, True))
