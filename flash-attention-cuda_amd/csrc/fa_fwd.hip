@@ -393,7 +393,7 @@ constexpr kernel_fn pick_kernel() {
 
 // W4: 4 waves x 64 query rows (one wave per SIMD), K/V double-buffered (64 KB)
 #define FA_CFG_W4D(ID, C, DT, HDIM, NAME)                                              \
-  {{ID, 256, 64, 4, C, 0, kW4LdsBytes, NAME, DT, HDIM}, 0, 5,                            \
+  {{ID, 256, 64, 4, C, 0, w4_lds_bytes<HDIM>(), NAME, DT, HDIM}, 0, 5,                   \
    pick_kernel<4, 64, C, 5, 0, DT, HDIM>()}
 #define FA_CFG_W4(ID, C, DT, NAME) FA_CFG_W4D(ID, C, DT, 128, NAME)
 // W4P: 4 waves x 16 query rows of each of two (G = 1) or four (G = 2) 64-row

@@ -337,6 +337,35 @@ class Stream:
         if k in ("dsr", "dsw"):
             self.lgkm.append((set(ins.w) if ins.lgkm_dst else None, self.pos - 1))
 
+    def far(self, cond, label):
+        """branch whose target may lie past the +-128 KiB of a SOPP branch
+        (the dbl programs): an inverted short branch over s_getpc_b64 +
+        pc-relative add + s_setpc_b64 (LLVM's own branch relaxation sequence;
+        s[58:59] are free in the key loop and at item boundaries)"""
+        inv = {"s_cbranch_scc0": "s_cbranch_scc1", "s_cbranch_scc1": "s_cbranch_scc0"}
+        skip = None
+        if cond != "s_branch":
+            skip = newlabel("nofar")
+            self.raw(f"{inv[cond]} {skip}")
+        post = newlabel("pc")
+        self.raw("s_getpc_b64 s[58:59]")
+        self.out.append(f"{post}:")
+        self.raw(f"s_add_u32 s58, s58, ({label}-{post})&4294967295")
+        self.raw(f"s_addc_u32 s59, s59, ({label}-{post})>>32")
+        self.raw("s_setpc_b64 s[58:59]")
+        self.pending.setdefault(label, []).append(self._snap())
+        if skip is None:
+            self.dead = True
+        else:
+            self.label(skip)
+
+    def jump(self, cond, label):
+        """a loop-control branch: far in the dbl programs"""
+        if dbl():
+            self.far(cond, label)
+        else:
+            self.branch(cond, label)
+
     def interleave(self, mfmas, gaps):
         """gaps[k] = fillers issued before mfmas[k]; gaps[len(mfmas)] after the last"""
         for k, m in enumerate(mfmas):
@@ -428,6 +457,50 @@ VBUF = [32768, 49152]
 KADDR = [f"%[ka{t}]" for t in range(4)]
 VADDR = ["%[va0]", "%[va1]"]
 
+# Two key tiles per barrier ("dbl", head_dim 128 non-split programs under
+# LDS-DMA): four K and four V images (K at 0..48K, V at 64K..112K, the item
+# table after them at 128K), tiles issued two ahead (K(j+3), V(j+2) in
+# iteration j), so an iteration of two steady tiles -- phase A(j), B(j),
+# A(j+1), B(j+1) -- needs one vmcnt wait and one barrier, and the second
+# phase A's first K fragments are read in the first phase B's tail.  The V
+# images' ds offsets exceed 16 bits from the lane bases, so the V bases are
+# copied + 64K into v188 / v189 (free under DMA staging), the prologue's V
+# write base into v190.
+DBL_XP = "dbl" in XP
+CUR = {"split": False}
+
+
+def dbl():
+    return DBL_XP and DMA_ON and HDC["hd"] == 128 and not CUR["split"]
+
+
+def nbuf():   # K / V images per tensor
+    return 4 if dbl() else 2
+
+
+def look():   # tiles a DMA runs ahead of the iteration that reads them
+    return 2 if dbl() else 1
+
+
+def kbuf(i):  # ds offset of tile i's K image (from the %[ka*] lane bases)
+    return 16384 * (i % nbuf())
+
+
+def vbuf(i):  # ds offset of tile i's V image (from vaddr())
+    return 16384 * (i % 4) if dbl() else VBUF[i % 2]
+
+
+def vbuf_abs(i):  # LDS byte offset of tile i's V image (M0 of its DMA)
+    return 65536 + 16384 * (i % 4) if dbl() else VBUF[i % 2]
+
+
+def vaddr(k):
+    return ("v188", "v189")[k] if dbl() else VADDR[k]
+
+
+def vlds():
+    return "v190" if dbl() else "%[vlds]"
+
 # scalar scratch (clobbered): staging descriptors and loop state
 SK = "s[40:43]"      # K stage descriptor (tile j+3 in iteration j)
 SV = "s[44:47]"      # V stage descriptor (tile j+2)
@@ -442,6 +515,7 @@ RQ, RO, RL = "s[72:75]", "s[76:79]", "s[80:83]"   # Q / O of the head, split: LS
 NX = "s[84:87]"             # scratch descriptor for the next item's prefetch
 QW, QM, NTILES, KVHI = "s88", "s89", "s90", "s91"  # this wave's first row, mask coordinate
 ITEM, WARM = "s92", "s93"   # item index; 1 if this item's Q, K(0), V(0), K(1) were prefetched
+SNWMIN = "s71"              # dbl: the item's smallest n_w over the four waves (PEND's slot: RSA is off)
 
 
 def kslot(cb, t):
@@ -459,7 +533,7 @@ def k_read(t, cb, slot, kb):
 
 def v_reads(u, e, slot, vb):
     off = vb + 32 * ROWB() * u + 512 * (e >> 1)
-    a = VADDR[e & 1]
+    a = vaddr(e & 1)
     return [dsr(f"ds_read_b64_tr_b16 {VF(slot, 0)}, {a} offset:{off}", VF(slot, 0), a),
             dsr(f"ds_read_b64_tr_b16 {VF(slot, 1)}, {a} offset:{off + 16 * ROWB()}", VF(slot, 1), a)]
 
@@ -615,16 +689,17 @@ def stage_writes(p):
 
 
 def dma_loads(p):
-    """LDS-DMA of K(j+2) -> kbuf[p] and V(j+1) -> vbuf[1-p] (iteration j, p = j&1):
-    wave w's piece i of a tile is LDS bytes [4096w + 1024i, +1024), M0 set per
-    piece (one MFMA between the M0 write and the load: its wait state); then
-    the descriptors advance one tile"""
+    """LDS-DMA of K(j+1+look) and V(j+look) into their images (iteration j,
+    p = j mod nbuf; two images per tensor: K(j+2) -> kbuf[p], V(j+1) ->
+    vbuf[1-p]): wave w's piece i of a tile is LDS bytes [4096w + 1024i,
+    +1024), M0 set per piece (one MFMA between the M0 write and the load: its
+    wait state); then the descriptors advance one tile"""
     out = []
     for i in range(npiece()):
-        out.append(salu(f"s_add_u32 m0, %[dmab], {KBUF[p] + 1024 * i}"))
+        out.append(salu(f"s_add_u32 m0, %[dmab], {kbuf(p + 1 + look()) + 1024 * i}"))
         out.append(vmem(f"buffer_load_dwordx4 {KD(i)}, {SK}, 0 offen lds", r=[KD(i)]))
     for i in range(npiece()):
-        out.append(salu(f"s_add_u32 m0, %[dmab], {VBUF[1 - p] + 1024 * i}"))
+        out.append(salu(f"s_add_u32 m0, %[dmab], {vbuf_abs(p + look()) + 1024 * i}"))
         out.append(vmem(f"buffer_load_dwordx4 {VD(i)}, {SV}, 0 offen lds", r=[VD(i)]))
     tb = hex(TILEB())
     out += [salu(f"s_add_u32 s40, s40, {tb}"), salu("s_addc_u32 s41, s41, 0"),
@@ -682,7 +757,40 @@ def lag():
     return 2 if NT() == 4 else 3
 
 
-def phase_a(st, p, with_max, diag=False):
+# bf16 scores in fp32 (verdict r05 item 5): the bf16 programs take Q into
+# the MFMA unscaled (exact), start each chain from C = -m_ref / c and
+# multiply every score by c = log2(e)/sqrt(d) in fp32 after its chain --
+# instead of a bf16-rounded Q * c (8 mantissa bits: 4.3-5.2e-3 max error on
+# peaked inputs against SDPA's 1.4-1.5e-3, profiles/r05_bf16_peaked_err.jsonl).
+# fp16 keeps Q * c (11 bits: within the oracle gate).  W4_XP=bf16q: the old
+# bf16 form, for A/B.
+BF16_FP32SCALE = "bf16q" not in XP
+
+
+def fp32scale():
+    return BF16_FP32SCALE and DT.get("bf16", False)
+
+
+def c_lits():
+    """(c, -1/c) as fp32 hex literals, c = fp32(1/sqrt(hd)) * fp32(log2 e) as
+    fa_fwd.hip computes p.c"""
+    import struct
+    import numpy as np
+    hd = HDC["hd"]
+    c = np.float32(np.float32(1.0) / np.sqrt(np.float32(hd))) * np.float32(1.4426950408889634)
+    ni = np.float32(-1.0) / np.float32(c)
+    h = lambda x: "0x%08x" % struct.unpack("<I", struct.pack("<f", float(x)))[0]  # noqa: E731
+    return h(c), h(ni)
+
+
+def scale_ops(b, cb):
+    """S(b, cb) *= c in fp32 (fp32scale)"""
+    cl = c_lits()[0]
+    x = 16 * b + 4 * cb
+    return [valu(f"v_mul_f32_e32 v{x + i}, {cl}, v{x + i}", r=[f"v{x + i}"], w=[f"v{x + i}"]) for i in range(4)]
+
+
+def phase_a(st, p, with_max, diag=False, k0_issued=False):
     """QK^T(j+1) from kbuf[(j+1)&1] beside cvt P(j), maxima of S(j+1), staging.
     diag: the wave's causal diagonal tile with its keys aligned to its rows
     (kv0 = qm, a whole tile before kv_hi): 16-row block (b, cb) is all valid
@@ -690,7 +798,7 @@ def phase_a(st, p, with_max, diag=False):
     scores set to -inf), and masked per element on it (key 4sg + i > row r16)
     -- the general mask_last_tile + full_max path, block by block, beside
     the 40 remaining MFMAs"""
-    kb = KBUF[1 - p]
+    kb = kbuf(p + 1)
     chains = [(b, cb) for cb in range(4) for b in range(4) if not diag or cb <= b]
     mf = []
     if "tmajor" in XP:
@@ -725,6 +833,8 @@ def phase_a(st, p, with_max, diag=False):
         for ins in k0:
             st.emit(ins)
         flush_rowsums(st)
+    elif k0_issued:
+        pass  # read in the previous phase B's tail (dbl: no barrier between)
     elif NT() == 2 or "kpre" not in XP or diag or not with_max:
         put(0, k0)
     if diag:
@@ -771,6 +881,8 @@ def phase_a(st, p, with_max, diag=False):
                 put(NT() * x + 1 + t % 3, k_read(t, cb + 1, kslot(cb + 1, t), kb))
         # the running maxima of chain x - LAG (its MFMA results clear of the
         # 12-wait-state MFMA -> VALU window)
+        if fp32scale() and with_max and x >= lag() and "nomax" not in XP:
+            put(NT() * x + MAX_OFF - 1, scale_ops(*chains[x - lag()]))
         if with_max and x >= lag() and "nomax" not in XP:
             y = x - lag()
             by, cby = chains[y]
@@ -798,11 +910,15 @@ def phase_a(st, p, with_max, diag=False):
     # the first V^T fragments of PV(j) (V(j) is ready since the last barrier)
     if "vinA" in XP and with_max and not diag:  # timing only: all 16, spread over phase A
         for f in range(16):
-            for i, r in enumerate(v_reads(f // 8, f % 8, f % 8, VBUF[p])):
+            for i, r in enumerate(v_reads(f // 8, f % 8, f % 8, vbuf(p))):
                 put(6 + 3 * f + i, r)
     for f in range(vahead()):
-        for i, r in enumerate(v_reads(*divmod(f, NE()), vslot(f), VBUF[p])):
+        for i, r in enumerate(v_reads(*divmod(f, NE()), vslot(f), vbuf(p))):
             put(n - 12 - 3 * (vahead() - 3) + 3 * f + i, r)
+    if fp32scale():
+        rest = chains[len(chains) - lag():] if with_max and "nomax" not in XP else chains
+        for y in rest:
+            put(n, scale_ops(*y))
     assert max(gaps) <= n, "every filler lands in a gap"
     st.interleave(mf, gaps)
     leftover = []
@@ -813,9 +929,11 @@ def phase_a(st, p, with_max, diag=False):
     return leftover
 
 
-def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
-    """PV(j) from vbuf[j&1]; decision at dec_gap; exp2 of S(j+1) after it"""
-    vb = VBUF[p]
+def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True, kpre=None):
+    """PV(j) from vbuf[j&1]; decision at dec_gap; exp2 of S(j+1) after it.
+    kpre (dbl): tile index whose K image the next phase A reads -- its first
+    key block's fragments are read in this phase's tail"""
+    vb = vbuf(p)
     mf, frag_first = pv_mfmas(rowsums=not (RSA and exps) and "norowsum" not in XP)
     gaps = {}
 
@@ -846,6 +964,11 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True):
     if "kpre" in XP and exps:  # timing only: next phase A's cb-0 K fragments (stale buffer)
         for t in range(4):
             put(len(mf) - 12 + 2 * t, k_read(t, 0, t, KBUF[p]))
+    if kpre is not None:
+        # the K fragments were consumed by the previous phase A: their slots
+        # are free; K(kpre) was published by the barrier before this phase
+        for t in range(NT()):
+            put(len(mf) - 10 + 2 * t, k_read(t, 0, kslot(0, t), kbuf(kpre)))
     # stage traffic (phase A is the denser half): LDS writes of stage j, then
     # the next stage's global loads, spread over the gaps after the decision
     if "nostage" not in XP and ("stage_a" not in XP or STAGE2):
@@ -969,7 +1092,10 @@ def shift_block(st, b, sh, first):
         st.emit(valu(f"v_sub_f32 {x}, {x}, {sh}", r=[x, sh], w=[x]))
     st.emit(valu(f"v_add_f32 {MREF[b]}, {MREF[b]}, {sh}", r=[MREF[b], sh], w=[MREF[b]]))
     for i in range(4):
-        st.emit(valu(f"v_xor_b32 {NEGM(b, i)}, 0x80000000, {MREF[b]}", r=[MREF[b]], w=[NEGM(b, i)]))
+        if fp32scale():
+            st.emit(valu(f"v_mul_f32_e32 {NEGM(b, i)}, {c_lits()[1]}, {MREF[b]}", r=[MREF[b]], w=[NEGM(b, i)]))
+        else:
+            st.emit(valu(f"v_xor_b32 {NEGM(b, i)}, 0x80000000, {MREF[b]}", r=[MREF[b]], w=[NEGM(b, i)]))
 
 
 _lbl = [0]
@@ -1063,7 +1189,7 @@ def qk_plain(st, kb):
 
 
 def pv_plain(st, p):
-    vb = VBUF[p]
+    vb = vbuf(p)
     mf, frag_first = pv_mfmas()
     gaps = {}
     for f in range(2 * NE()):
@@ -1074,8 +1200,38 @@ def pv_plain(st, p):
     st.interleave(mf, gaps)
 
 
+def double_steady(st, p, labels):
+    """dbl: steady tiles j and j+1 (j mod 4 = p) in one barrier interval --
+    phase A(j) [QK(j+1), DMA K(j+3) / V(j+2)], phase B(j) [PV(j); QK(j+2)'s
+    first K fragments in its tail], phase A(j+1) [QK(j+2), DMA K(j+4) /
+    V(j+3)], phase B(j+1) [PV(j+1)]; then one DMA wait and one barrier.  The
+    images it reads (K(j+1), K(j+2), V(j), V(j+1)) were published by the
+    previous barrier; the ones it fills were last read before it."""
+    L, nb = labels, nbuf()
+    q = (p + 1) % nb
+    left = phase_a(st, p, with_max=True)
+    stamp(st, 62)
+    stamp_acc(st, 64, 62, 60)
+    phase_b(st, p, left, dec_gap=6, label_slow=L["dslow1"][p], label_end=L["dmid"][p], kpre=p + 2)
+    st.label(L["dmid"][p])
+    left = phase_a(st, q, with_max=True, k0_issued=True)
+    stamp(st, 62)
+    stamp_acc(st, 64, 62, 60)
+    phase_b(st, q, left, dec_gap=6, label_slow=L["dslow2"][p], label_end=L["dend"][p])
+    st.label(L["dend"][p], drain_lgkm=True)
+    st.raw("s_waitcnt vmcnt(0)")
+    st.raw("s_barrier")
+    stamp(st, 62)
+    stamp_acc(st, 66, 62, 60)
+    st.raw(f"s_add_u32 {SJ}, {SJ}, 2")
+    st.raw(f"s_cmp_lt_u32 {SJ}, {NTILES}")
+    st.jump("s_cbranch_scc1", L["loop"][(p + 2) % nb])
+    st.jump("s_branch", L["done"])
+
+
 def body(st, p, causal, labels):
-    """one loop iteration j of parity p = j & 1"""
+    """one loop iteration j of parity p = j mod nbuf (dbl, odd p: two steady
+    tiles per barrier when both are steady)"""
     L = labels
     st.label(L["loop"][p], drain_lgkm=True)
     stamp(st, 60)
@@ -1085,6 +1241,16 @@ def body(st, p, causal, labels):
     st.raw(f"s_add_u32 {ST0}, {SJ}, 2")
     st.raw(f"s_cmp_eq_u32 {ST0}, {SMASKJ}")
     st.branch("s_cbranch_scc1", L["masked"][p])
+    if dbl() and p % 2 == 1:
+        # two tiles per barrier only where EVERY wave's tiles j and j+1 are
+        # steady (j + 3 < the smallest n_w: no wave drains or masks QK(j+1) /
+        # QK(j+2)) -- the choice must be the workgroup's, or the waves' barrier
+        # counts would part (causal waves have n_w = n_0 .. n_0 + 3)
+        st.raw(f"s_add_u32 {ST1}, {SJ}, 3")
+        st.raw(f"s_cmp_lt_u32 {ST1}, {SNWMIN}")
+        st.branch("s_cbranch_scc0", L["single"][p])
+        double_steady(st, p, labels)
+        st.label(L["single"][p])
     # ---- steady: QK(j+1) with maxima, PV(j) with exps ----
     left = phase_a(st, p, with_max=True)
     stamp(st, 62)
@@ -1203,10 +1369,10 @@ def body(st, p, causal, labels):
     stamp_acc(st, 66, 62, 60)
     st.raw(f"s_add_u32 {SJ}, {SJ}, 1")
     st.raw(f"s_cmp_lt_u32 {SJ}, {NTILES}")
-    if p == 0:
-        st.branch("s_cbranch_scc0", L["done"])
+    if p < nbuf() - 1:
+        st.jump("s_cbranch_scc0", L["done"])  # else on to body p + 1
     else:
-        st.branch("s_cbranch_scc1", L["loop"][0])
+        st.jump("s_cbranch_scc1", L["loop"][0])
 
 
 def prostamp(st, i):
@@ -1294,6 +1460,16 @@ def read_item(st, causal):
     else:
         st.raw(f"s_mov_b32 {SNW}, {NTILES}")
     st.raw(f"s_sub_u32 {SNW1}, {SNW}, 1")
+    if dbl():
+        # n_w of wave 0 (qm - woff): the workgroup's smallest
+        if causal:
+            st.raw(f"s_sub_i32 {SNWMIN}, {QM}, %[woff]")
+            st.raw(f"s_ashr_i32 {SNWMIN}, {SNWMIN}, 6")
+            st.raw(f"s_add_i32 {SNWMIN}, {SNWMIN}, 1")
+            st.raw(f"s_min_i32 {SNWMIN}, {SNWMIN}, {NTILES}")
+            st.raw(f"s_max_i32 {SNWMIN}, {SNWMIN}, 0")
+        else:
+            st.raw(f"s_mov_b32 {SNWMIN}, {SNW}")
     # the wave's last tile (key kv0 = 64 (n_w - 1)) needs a mask iff it
     # reaches the key bound or (causal) the diagonal: SMASKJ = n_w, else never
     st.raw(f"s_lshl_b32 {ST0}, {SNW}, 6")                 # kv0 + 64
@@ -1422,6 +1598,10 @@ def q_scale(st):
             for x in xs:
                 st.raw(f"v_accvgpr_write_b32 a{144 + x}, {pk[x]}")
             continue
+        if fp32scale():  # Q unscaled: c applies to the fp32 scores
+            for x in xs:
+                st.raw(f"v_accvgpr_write_b32 a{144 + x}, v{x}")
+            continue
         if DT["bf16"]:
             for x in xs:  # bf16 -> fp32 is exact: the 16 bits move to the top half
                 st.raw(f"v_lshlrev_b32_e32 {lo[x]}, 16, v{x}")
@@ -1520,8 +1700,24 @@ def prologue(st, causal, split=False):
         # previous item's last barrier freed every image
         st.raw(f"s_waitcnt vmcnt({sg0()})")
         for i in range(NPASS()):
-            st.raw(f"ds_write_b128 %[vlds], {vst(i, 1)} offset:{VBUF[0] + PASSL() * i}")
+            st.raw(f"ds_write_b128 {vlds()}, {vst(i, 1)} offset:{vbuf(0) + PASSL() * i}")
             st.raw(f"ds_write_b128 %[klds], {kst(i, 1)} offset:{KBUF[1] + PASSL() * i}")
+    if dbl():
+        # two tiles ahead: K(2), V(1) by LDS-DMA now (the previous item's last
+        # barrier freed their images); iteration 0's end waits for them
+        for i in range(npiece()):
+            st.raw(f"s_add_u32 m0, %[dmab], {kbuf(2) + 1024 * i}")
+            st.nop(1)
+            st.raw(f"buffer_load_dwordx4 {KD(i)}, {SK}, 0 offen lds")
+        for i in range(npiece()):
+            st.raw(f"s_add_u32 m0, %[dmab], {vbuf_abs(1) + 1024 * i}")
+            st.nop(1)
+            st.raw(f"buffer_load_dwordx4 {VD(i)}, {SV}, 0 offen lds")
+        tb = hex(TILEB())
+        for ins in (f"s_add_u32 s40, s40, {tb}", "s_addc_u32 s41, s41, 0", f"s_sub_i32 {SKREM}, {SKREM}, {tb}",
+                    f"s_max_i32 s42, {SKREM}, 0", f"s_add_u32 s44, s44, {tb}", "s_addc_u32 s45, s45, 0",
+                    f"s_sub_i32 {SVREM}, {SVREM}, {tb}", f"s_max_i32 s46, {SVREM}, 0"):
+            st.raw(ins)
     prostamp(st, 1)  # -> K(0) written, Q scaled
     st.raw("s_waitcnt lgkmcnt(0)")
     st.raw("s_barrier")
@@ -1538,6 +1734,11 @@ def prologue(st, causal, split=False):
         st.label(s0done)
     else:
         qk_plain(st, KBUF[0])
+    if fp32scale():
+        for b in range(4):
+            for cb in range(4):
+                for ins in scale_ops(b, cb):
+                    st.emit(ins)
     prostamp(st, 2)  # -> S(0) (+ the deferred epilogue) done
     st.raw(f"s_cmp_eq_u32 {SMASKJ}, 1")
     skip = newlabel("nomask0")
@@ -1568,7 +1769,7 @@ def prologue(st, causal, split=False):
         st.raw(f"s_waitcnt vmcnt({sg0()})")
     if not (onebar()):
         for i in range(NPASS()):
-            st.raw(f"ds_write_b128 %[vlds], {vst(i, 1)} offset:{VBUF[0] + PASSL() * i}")
+            st.raw(f"ds_write_b128 {vlds()}, {vst(i, 1)} offset:{vbuf(0) + PASSL() * i}")
             st.raw(f"ds_write_b128 %[klds], {kst(i, 1)} offset:{KBUF[1] + PASSL() * i}")
         st.raw("s_waitcnt lgkmcnt(0)")
         st.lgkm = []
@@ -1724,11 +1925,16 @@ def s0_with_epilogue(st):
 
 
 def generate(causal, split=False):
+    CUR["split"] = split
+    assert not (dbl() and (v14() or RSA or DIAG == "prostamps" or "epiwait16" in XP)), \
+        "dbl uses v188-v190 and s71 (PEND)"
     st = Stream()
-    labels = {k: [newlabel(f"{k}{p}") for p in range(2)]
-              for k in ("loop", "notsteady", "masked", "general", "slow", "slow2", "slow3", "end")}
-    labels["last"] = [newlabel(f"last{p}") for p in range(2)]
-    labels["end_nowait"] = [newlabel(f"endnw{p}") for p in range(2)]
+    nb = nbuf()
+    labels = {k: [newlabel(f"{k}{p}") for p in range(nb)]
+              for k in ("loop", "notsteady", "masked", "general", "slow", "slow2", "slow3", "end",
+                        "single", "dmid", "dend", "dslow1", "dslow2")}
+    labels["last"] = [newlabel(f"last{p}") for p in range(nb)]
+    labels["end_nowait"] = [newlabel(f"endnw{p}") for p in range(nb)]
     labels["done"] = newlabel("done")
     item = newlabel("item")
     # the workgroup's items (a chunk of fa_w4_kernel.hpp's table) in one
@@ -1744,6 +1950,10 @@ def generate(causal, split=False):
     st.raw(f"s_mov_b32 {WARM}, 0")
     if dma():
         dma_setup(st)
+    if dbl():
+        st.raw("v_add_u32 v188, 0x10000, %[va0]")
+        st.raw("v_add_u32 v189, 0x10000, %[va1]")
+        st.raw("v_add_u32 v190, 0x10000, %[vlds]")
     if DIAG == "prostamps":
         for r in range(200, 208):
             st.raw(f"v_mov_b32 v{r}, 0")
@@ -1753,8 +1963,8 @@ def generate(causal, split=False):
         st.raw("v_add_u32 v206, 1, v206")
     read_item(st, causal)
     prologue(st, causal, split)
-    body(st, 0, causal, labels)
-    body(st, 1, causal, labels)
+    for p in range(nb):
+        body(st, p, causal, labels)
     st.label(labels["done"], drain_lgkm=True)
     prostamp(st, 5)  # loop (every iteration incl. the last one's prefetch)
     pstamp(st, 64)
@@ -1768,7 +1978,11 @@ def generate(causal, split=False):
             st.raw(f"s_mov_b32 s{60 + i}, s{76 + i}")
         st.raw(f"s_lshl_b32 {ROWSAVE}, {QW}, {ROWSH()}")
         st.raw(f"s_mov_b32 {ITEM}, {ST0}")
-        st.raw(f"s_branch {item}")
+        if dbl():
+            st.far("s_branch", item)
+            st.dead = False  # (the label below is reached by its own branch)
+        else:
+            st.raw(f"s_branch {item}")
         st.label(last)
     # ST1 = qw * row bytes: the epilogue's row base
     st.raw(f"s_lshl_b32 {ST1}, {QW}, {ROWSH()}")
@@ -1808,9 +2022,10 @@ def generate(causal, split=False):
         st.nop(2)
     st.raw(f"s_add_u32 {ITEM}, {ITEM}, 1")
     st.raw(f"s_cmp_lt_u32 {ITEM}, %[nitems]")
-    st.branch("s_cbranch_scc1", item)
+    st.jump("s_cbranch_scc1", item)
     if dma():
         st.raw(f"s_mov_b32 m0, {SM0}")
+    CUR["split"] = False
     return st.out
 
 
@@ -1819,6 +2034,12 @@ HEADER = """// GENERATED by gen_w4_item.py -- do not edit.
 // see the generator's docstring for the register map and the schedule.
 #pragma once
 """
+
+
+def header():
+    # the head_dim-128 persistent programs' LDS layout (fa_w4_kernel.hpp):
+    # 1 = four K / V images per tensor and the item table at 128 KiB (dbl)
+    return HEADER + f"#define FA_W4_DBL {1 if DBL_XP and DMA_ON else 0}\n"
 
 
 def cxx(causal, bf16, lines, split=False):
@@ -1849,7 +2070,7 @@ __device__ __forceinline__ void {name}(const W4Run& rn, const W4Lane& ln) {{
 
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else "fa_w4_item.inc"
-    text = HEADER
+    text = header()
     for bf16 in (False, True):
         set_dtype(bf16)
         for causal in (False, True):

@@ -60,6 +60,20 @@ def set_hd(hd):
     w4.set_hd(hd)
 RESCALE = "0x41000000"  # 8.0: m_ref moves when a row max grew past it (log2 units)
 
+
+def fp32scale():
+    """bf16 scores in fp32, as gen_w4_item.fp32scale: Q unscaled into the
+    MFMA, NEGM = -m_ref / c, every score times c after its chain"""
+    return w4.BF16_FP32SCALE and DT.get("bf16", False)
+
+
+def scale_ops(b, cb):
+    """S(b, cb) *= c in fp32 (four scalar multiplies: packed fp32 VALU beside
+    MFMAs costs more issue, MI355X_MICROARCH.md constants table)"""
+    cl = w4.c_lits()[0]
+    x = 16 * b + 4 * cb
+    return [valu(f"v_mul_f32_e32 v{x + i}, {cl}, v{x + i}", r=[f"v{x + i}"], w=[f"v{x + i}"]) for i in range(4)]
+
 # ---------------------------------------------------------------------------
 # register map (VGPR v0-v213, AGPR a0-a239; the compiler keeps the rest)
 # ---------------------------------------------------------------------------
@@ -338,6 +352,8 @@ def phase_a(st, p, nq, np_):
                 put(NT * x + 1 + t % 3, k_read(t, cb + 1, kb))
         if x >= lag():
             by, cby = chains[x - lag()]
+            if fp32scale():
+                put(min(NT * x + MAX_OFF - 1, n), scale_ops(by, cby))
             mm = max_block(by, cby, first=(cby == 0))
             put(min(NT * x + MAX_OFF, n), mm[0])
             put(min(NT * x + MAX_OFF + 1, n), mm[1])
@@ -368,6 +384,9 @@ def phase_a(st, p, nq, np_):
     for f in range(va):
         for i, r in enumerate(v_reads(f, VBUF[p])):
             put(min(max(0, n - 2 * va) + 2 * f + i, n), r)
+    if fp32scale():
+        for y in range(max(0, len(chains) - lag()), len(chains)):
+            put(n, scale_ops(*chains[y]))
     assert max(gaps) <= n, "every filler lands in a gap"
     st.interleave(mf, gaps)
     left = []
@@ -527,7 +546,10 @@ def shift_block(st, b, sh, first):
         st.emit(valu(f"v_sub_f32 {x}, {x}, {sh}", r=[x, sh], w=[x]))
     st.emit(valu(f"v_add_f32 {MREF[b]}, {MREF[b]}, {sh}", r=[MREF[b], sh], w=[MREF[b]]))
     for i in range(4):
-        st.emit(valu(f"v_xor_b32 {NEGM(b, i)}, 0x80000000, {MREF[b]}", r=[MREF[b]], w=[NEGM(b, i)]))
+        if fp32scale():
+            st.emit(valu(f"v_mul_f32_e32 {NEGM(b, i)}, {w4.c_lits()[1]}, {MREF[b]}", r=[MREF[b]], w=[NEGM(b, i)]))
+        else:
+            st.emit(valu(f"v_xor_b32 {NEGM(b, i)}, 0x80000000, {MREF[b]}", r=[MREF[b]], w=[NEGM(b, i)]))
 
 
 def mask_block(st, b, causal):
@@ -615,6 +637,10 @@ def q_scale(st):
                     st.raw(op.text)
             for x in xs:
                 st.raw(f"v_accvgpr_write_b32 a{144 + x}, {pk[x]}")
+            continue
+        if fp32scale():  # Q unscaled: c applies to the fp32 scores
+            for x in xs:
+                st.raw(f"v_accvgpr_write_b32 a{144 + x}, v{x}")
             continue
         if DT["bf16"]:
             for x in xs:
@@ -723,6 +749,12 @@ def prologue(st, causal):
         qk_plain(st, KBUF[0], nb)
         st.branch("s_branch", s0done)
     st.label(s0done)
+    if fp32scale():
+        # every block's S(0) (the blocks without a tile hold zeros: harmless)
+        for b in range(NB):
+            for cb in range(4):
+                for ins in scale_ops(b, cb):
+                    st.emit(ins)
     st.raw(f"s_mov_b32 {KV0}, 0")
     first_done = w4.newlabel("firstdone")
     for b in range(NB):

@@ -16,7 +16,9 @@ from typing import List, Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libfa_mi355x.so")
+# FA_MI355X_LIB: another in-tree build of the library (experiment variants,
+# tools/w4_variant.sh) for a test or tool run; default the product library
+LIB_PATH = os.environ.get("FA_MI355X_LIB") or os.path.join(PKG_ROOT, "lib", "libfa_mi355x.so")
 
 HEAD_DIM = 128
 

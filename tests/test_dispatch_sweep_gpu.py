@@ -8,8 +8,11 @@ workspace-free C entry (`fa_fwd_f16` / `fa_fwd_bf16`, what the reference's
 The per-tier tests force one config each; this file checks that the
 dispatcher's choice (`fa_select_config`, the split / pool / W4P / W4 /
 KV-pair / KV-quad / loop boundaries in fa_fwd.hip) is right wherever it
-lands: every shape must match at 1e-3 (fp16) or 5e-3 (bf16), whichever tier
-runs it.
+lands: every shape must match at 1e-3 (fp16) or 2.5e-3 (bf16), whichever
+tier runs it.  Since round 6 every bf16 tier scales the fp32 scores by
+log2(e)/sqrt(d) instead of feeding a bf16-rounded Q * scale to the MFMA, so
+bf16 is gated against the plain fp32 model on peaked inputs too (round 5:
+5e-3 against a model with that rounding, 1e-2 against the plain one).
 """
 import math
 
@@ -60,15 +63,10 @@ BOUNDARY = [
 ]
 
 
-def _ref(q, k, v, causal, qc_bf16=False):
-    """fp32 attention of the 16-bit inputs; qc_bf16: with Q * scale * log2(e)
-    rounded to bf16 first -- the product every bf16 tier feeds its QK^T MFMA,
-    the one rounding the kernels add to the fp32 model"""
+def _ref(q, k, v, causal):
+    """fp32 attention of the 16-bit inputs"""
     b, h, s, d = q.shape
     qf = q.float()
-    if qc_bf16:
-        c = math.log2(math.e) / math.sqrt(d)
-        qf = (qf * c).to(torch.bfloat16).float() / c
     out = torch.empty((b, h, s, d), dtype=torch.float32, device=q.device)
     mask = torch.ones((s, s), dtype=torch.bool, device=q.device).tril() if causal else None
     for bi in range(b):
@@ -92,15 +90,12 @@ def _run(shape, seed, scale=1.0):
     fa = _fa()
     b, h, s, d, causal, bf16 = shape
     dtype = torch.bfloat16 if bf16 else torch.float16
-    tol = 5e-3 if bf16 else 1e-3
+    # bf16: P and O round to 8 significant bits (O on [-0.5, 0.5]: half an
+    # ulp is ~1e-3); the scores stay fp32 (round 5's bf16 Q * scale gave
+    # 4.3-5.2e-3 on peaked inputs, profiles/r05_bf16_peaked_err.jsonl)
+    tol = 2.5e-3 if bf16 else 1e-3
     q, k, v = _inputs(b, h, s, d, dtype, seed, scale)
-    # bf16 on peaked inputs: Q * scale rounded to bf16 (2^-9 relative) moves a
-    # score of 20 log2 units by 0.04 -- 2.7 % on its weight -- which alone
-    # gives ~4.5e-3 at q, k on [-3, 3] (profiles/r05_bf16_peaked_err.jsonl);
-    # the kernels are gated against the model with that rounding at 5e-3 and
-    # against the plain fp32 model at 1e-2
-    model = bf16 and scale > 1.0
-    ref = _ref(q, k, v, causal, qc_bf16=model)
+    ref = _ref(q, k, v, causal)
     # the Python / torch path: workspace entry
     o1 = fa.flash_attention_fwd(q, k, v, causal)
     torch.cuda.synchronize()
@@ -116,10 +111,6 @@ def _run(shape, seed, scale=1.0):
     err2 = (o2.float() - ref).abs().max().item()
     cfg = fa.configs()[fa.select_config(b, h, s, causal)].name if d == 128 and not bf16 else "-"
     assert err1 <= tol and err2 <= tol, (shape, cfg, err1, err2)
-    if model:
-        plain = _ref(q, k, v, causal)
-        assert (o1.float() - plain).abs().max().item() <= 1e-2
-        assert (o2.float() - plain).abs().max().item() <= 1e-2
 
 
 @pytest.mark.parametrize("shape", _random_shapes(40, 2028), ids=lambda s: "x".join(map(str, s)))
