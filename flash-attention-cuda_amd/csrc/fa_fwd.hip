@@ -872,7 +872,9 @@ static SplitPlan split_plan(int batch, int heads, int seq_len, int head_dim, int
 template <bool BF16>
 static int launch_split(const SplitPlan& sp, const void* q, const void* k, const void* v, void* o,
                         int bh, int seq_len, void* ws, hipStream_t stream) {
-  constexpr int kLds = kW4LdsBytes;  // K/V images + the one-slot item table
+  // K/V images + the item table, as the non-split program lays them out (a
+  // one-piece query block runs it)
+  constexpr int kLds = w4_lds_bytes<128>();
   static std::once_flag flags[64];
   static hipError_t errs[64];
   int dev = 0;

@@ -282,6 +282,10 @@ struct M16 {
   static constexpr int RW = 16 * QB;   // query rows per wave
   typedef typename Elem<T>::x8 tx8;
   typedef typename Elem<T>::x4 tx4;
+  // bf16: Q enters the MFMA unscaled and the fp32 scores are multiplied by c
+  // (C = -m_ref / c): a bf16-rounded Q * c (8 mantissa bits) cost 3x SDPA's
+  // error on peaked inputs.  fp16 keeps Q * c.
+  static constexpr bool kScaleS = std::is_same<T, __bf16>::value;
   int lane, r16, g, sg;
   int kaddr[4], vaddr[2];
   tx8 qf[QB][NTQ];
@@ -328,6 +332,10 @@ struct M16 {
             tx8, buf_load16(rq, (qw + 16 * b + r16) * ROW + (4 * t + g) * 16));
   }
   __device__ __forceinline__ void scale_q() {
+    if constexpr (kScaleS) {
+      pin_q();
+      return;
+    }
 #pragma unroll
     for (int b = 0; b < QB; ++b)
 #pragma unroll
@@ -359,7 +367,8 @@ struct M16 {
       for (int t = 0; t < NTQ; ++t)
         if ((b * NTQ + t) % NPART == j) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) qf[b][t][e] = (T)((float)qf[b][t][e] * c);
+          for (int e = 0; e < 8; ++e)
+            if constexpr (!kScaleS) qf[b][t][e] = (T)((float)qf[b][t][e] * c);
           reinterpret_cast<tx8*>(region)[(b * NTQ + t) * 64 + lane] = qf[b][t];
         }
   }
@@ -427,6 +436,12 @@ struct M16 {
   }
   template <bool CAUSAL>
   __device__ __forceinline__ void softmax(int kv0, int kv_hi, int qw, float /*c*/, bool need_mask) {
+    if constexpr (kScaleS) {
+#pragma unroll
+      for (int b = 0; b < QB; ++b)
+#pragma unroll
+        for (int cb = 0; cb < NKB; ++cb) s[b][cb] *= c;
+    }
     if (need_mask) {
 #pragma unroll
       for (int b = 0; b < QB; ++b) {
@@ -476,7 +491,8 @@ struct M16 {
 #pragma unroll
         for (int cb = 0; cb < NKB; ++cb) s[b][cb] -= sh;
         m_ref[b] += sh;
-        negm[b] = f32x4{-m_ref[b], -m_ref[b], -m_ref[b], -m_ref[b]};
+        const float nm = kScaleS ? -m_ref[b] / c : -m_ref[b];
+        negm[b] = f32x4{nm, nm, nm, nm};
       }
       have_ref = true;
     }

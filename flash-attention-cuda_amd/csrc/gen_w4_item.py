@@ -466,7 +466,14 @@ VADDR = ["%[va0]", "%[va1]"]
 # images' ds offsets exceed 16 bits from the lane bases, so the V bases are
 # copied + 64K into v188 / v189 (free under DMA staging), the prologue's V
 # write base into v190.
-DBL_XP = "dbl" in XP
+# (default since round 6: bit-identical to the one-tile form, stamped tile
+# 2887 -> 2784 cycles at S=8192 non-causal, 2969 -> 2899 causal; same
+# process +1.0 % S=8192 non-causal, +0.75 % S=16384 causal, +0.3 % the
+# headline, level S=8192 causal -- the cycles return partly as clock,
+# profiles/r06_w4_dbl_stamps.jsonl, r06_ab_w4_dbl.jsonl; W4_XP=nodbl for A/B)
+# (off under the experiments that use v184-v207 or s71: v14, rsa, epiwait16,
+# prostamps)
+DBL_XP = "nodbl" not in XP and not ({"v14", "rsa", "epiwait16"} & XP) and DIAG != "prostamps"
 CUR = {"split": False}
 
 
@@ -963,7 +970,7 @@ def phase_b(st, p, leftover, dec_gap, label_slow, label_end, exps=True, kpre=Non
         put(LEFT_OFF + i, ins)
     if "kpre" in XP and exps:  # timing only: next phase A's cb-0 K fragments (stale buffer)
         for t in range(4):
-            put(len(mf) - 12 + 2 * t, k_read(t, 0, t, KBUF[p]))
+            put(len(mf) - 12 + 2 * t, k_read(t, 0, t, kbuf(p)))
     if kpre is not None:
         # the K fragments were consumed by the previous phase A: their slots
         # are free; K(kpre) was published by the barrier before this phase
@@ -1926,8 +1933,6 @@ def s0_with_epilogue(st):
 
 def generate(causal, split=False):
     CUR["split"] = split
-    assert not (dbl() and (v14() or RSA or DIAG == "prostamps" or "epiwait16" in XP)), \
-        "dbl uses v188-v190 and s71 (PEND)"
     st = Stream()
     nb = nbuf()
     labels = {k: [newlabel(f"{k}{p}") for p in range(nb)]
