@@ -42,7 +42,15 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import gen_w4_item as w4  # noqa: E402
 from gen_w4_item import DT, NINF, R, Stream, dsr, mfma, salu, set_dtype, valu, vmem  # noqa: E402
 
-NB = 4                 # query blocks per workgroup (at most)
+NB = 4                 # query blocks per workgroup (at most: the register map's)
+# blocks of the generated function: 4 (quads, G = 2) or 2 (pairs, G = 1: no
+# absent blocks' Q loads / scaling / O, l zeroing in the prologue, no
+# 3- and 4-block kinds; round 6)
+CURNB = {"nb": 4}
+
+
+def nb():
+    return CURNB["nb"]
 # head_dim of the generated function (set_hd: 128, the reference's, or 64):
 # k-steps of a QK^T chain, 16-column O blocks, bytes of a Q/K/V/O row (HBM
 # and the packed LDS images), of a 64-key tile, 1-KiB LDS-DMA pieces per wave
@@ -171,6 +179,13 @@ KVH = [f"%[kvh{b}]" for b in range(NB)]
 TB = [f"%[t{b}]" for b in range(NB)]
 
 MAX_OFF, LEFT_OFF, DEC_GAP = 2, 3, 6
+# prologue experiment (W4_XP=latev0k1): S(0) starts once Q and K(0) are in,
+# V(0) / K(1) written after S(0) and the first softmax, before the
+# prologue's second barrier.  Measured and not kept: the prologue stays at
+# 7.0k cycles and the launches are level to slower (config 1 534.2 vs
+# 537.7, B=2 S=1024 causal 677.2 vs 697.9, H=16 S=2048 957.5 vs 972.8;
+# S=2048 causal 882.6 vs 870.8; profiles/r06_ab_w4p_prologue_nolds.jsonl)
+LATE_V0K1 = "latev0k1" in w4.XP
 
 
 def lag():  # chains between a chain and its maxima (a chain is NT MFMAs)
@@ -597,16 +612,44 @@ def qk_plain(st, kb, nb):
 
 
 # iteration kinds (NP, NQ): steady, one block's drain, every block's drain
-KINDS = [(k, k) for k in range(1, NB + 1)] + [(k, k - 1) for k in range(1, NB + 1)] + \
-        [(k, 0) for k in range(2, NB + 1)]
+def kinds():
+    n = nb()
+    return [(k, k) for k in range(1, n + 1)] + [(k, k - 1) for k in range(1, n + 1)] + \
+        [(k, 0) for k in range(2, n + 1)]
 
 
 def kname(np_, nq):
     return f"k{np_}{nq}"
 
 
+class _NoLds:
+    """timing-only probe (W4_XP=p1nolds, wrong results): the one-block
+    iterations issue no LDS reads (K and V^T fragments stay stale) -- what
+    the iteration costs without its 128 KiB per CU of fragment reads"""
+
+    def __init__(self, st):
+        self.st = st
+
+    def emit(self, ins):
+        if isinstance(ins, str) or ins.kind != "dsr":
+            self.st.emit(ins)
+
+    def interleave(self, mfmas, gaps):
+        for k, m in enumerate(mfmas):
+            for f in gaps.get(k, []):
+                self.emit(f)
+            self.emit(m)
+        for f in gaps.get(len(mfmas), []):
+            self.emit(f)
+
+    def __getattr__(self, k):
+        return getattr(self.st, k)
+
+
 def iteration(st, p, np_, nq, causal, Lb):
     stamp_path(st, NB - nq if nq else NPATH - 1)   # 0: 4 QK blocks .. 3: 1; 4: drain
+    if "p1nolds" in w4.XP and np_ == 1:
+        st = _NoLds(st)
     left, late = phase_a(st, p, nq, np_)
     mask_pass(st, nq, causal)
     phase_b(st, p, nq, np_, left, Lb["slow_" + kname(np_, nq)][p], Lb["end"][p], late)
@@ -625,7 +668,7 @@ def rsrc(st, dst, lo, hi, records):
 def q_scale(st):
     """Q * c (fp32 product, then fp16: M16::scale_q) from v0-63 into a144-207,
     eight elements at a time in the (free) V^T fragment registers"""
-    qregs = [16 * b + j for b in range(NB) for j in range(4 * NT)]  # Q(b, t) raw: v[16b + 4t ..]
+    qregs = [16 * b + j for b in range(nb()) for j in range(4 * NT)]  # Q(b, t) raw: v[16b + 4t ..]
     for c0 in range(0, len(qregs), 8):
         xs = qregs[c0:c0 + 8]
         lo = {x: f"v{144 + 3 * i}" for i, x in enumerate(xs)}
@@ -693,13 +736,13 @@ def prologue(st, causal):
     rsrc(st, 44, "%[vlo]", "%[vhi]", "%[kvrec]")
     rsrc(st, 60, "%[olo]", "%[ohi]", "%[qrec]")
     # Q rows qr_b + r16, chunk g of k-step t: (qr_b << 8) + qoff + 64 t
-    for b in range(NB):
+    for b in range(nb()):
         st.raw(f"s_lshl_b32 {ST0}, {QR[b]}, {ROWSH}")
         st.raw(f"v_add_u32 {T[b]}, {ST0}, %[qoff]")
     for i in range(NPIECE):
         st.raw(f"v_add_u32 {T[4 + i]}, {hex(TILEB)}, {KOFF[i]}")
     st.nop(5)
-    for b in range(NB):
+    for b in range(nb()):
         for t in range(NT):
             st.raw(f"buffer_load_dwordx4 {R('v', 16 * b + 4 * t, 4)}, {T[b]}, {RQ}, 0 offen offset:{64 * t}")
     for i in range(NPIECE):
@@ -718,46 +761,47 @@ def prologue(st, causal):
     st.raw("s_addc_u32 s45, s45, 0")
     st.raw(f"s_sub_i32 {SVREM}, s46, {t1}")
     st.raw(f"s_max_i32 s46, {SVREM}, 0")
-    # O, l, -m_ref, m_ref = 0
-    for x in range(144):
+    # O, l, -m_ref, m_ref = 0 (the function's blocks)
+    for x in list(range(32 * nb())) + list(range(128, 128 + 4 * nb())):
         st.raw(f"v_accvgpr_write_b32 a{x}, 0")
-    for x in range(96, 112):
+    for x in range(96, 96 + 4 * nb()):
         st.raw(f"v_mov_b32 v{x}, 0")
-    for b in range(NB):
+    for b in range(nb()):
         st.raw(f"v_mov_b32 {MREF[b]}, 0")
     # Q and K(0) landed; V(0), K(1) may still fly
     st.raw(f"s_waitcnt vmcnt({2 * NPIECE})")
     for i in range(NPIECE):
         st.raw(f"ds_write_b128 %[klds], {KF(i)} offset:{KBUF[0] + PASSL * i}")
     q_scale(st)
-    st.raw("s_waitcnt vmcnt(0)")
-    for i in range(NPIECE):
-        st.raw(f"ds_write_b128 %[vlds], {VST1(i)} offset:{VBUF[0] + PASSL * i}")
-        st.raw(f"ds_write_b128 %[klds], {KST1(i)} offset:{KBUF[1] + PASSL * i}")
+    if not LATE_V0K1:
+        st.raw("s_waitcnt vmcnt(0)")
+        for i in range(NPIECE):
+            st.raw(f"ds_write_b128 %[vlds], {VST1(i)} offset:{VBUF[0] + PASSL * i}")
+            st.raw(f"ds_write_b128 %[klds], {KST1(i)} offset:{KBUF[1] + PASSL * i}")
     st.raw("s_waitcnt lgkmcnt(0)")
     st.raw("s_barrier")
     st.nop(2)
     # S(0) of the blocks with a tile (a prefix: T sorted descending)
     s0done = w4.newlabel("s0done")
-    lbl = {nb: w4.newlabel(f"s0n{nb}") for nb in range(1, NB + 1)}
-    for nb in range(NB, 1, -1):
-        st.raw(f"s_cmp_lg_u32 {TB[nb - 1]}, 0")
-        st.branch("s_cbranch_scc1", lbl[nb])
+    lbl = {n: w4.newlabel(f"s0n{n}") for n in range(1, nb() + 1)}
+    for n in range(nb(), 1, -1):
+        st.raw(f"s_cmp_lg_u32 {TB[n - 1]}, 0")
+        st.branch("s_cbranch_scc1", lbl[n])
     st.branch("s_branch", lbl[1])
-    for nb in range(NB, 0, -1):
-        st.label(lbl[nb])
-        qk_plain(st, KBUF[0], nb)
+    for n in range(nb(), 0, -1):
+        st.label(lbl[n])
+        qk_plain(st, KBUF[0], n)
         st.branch("s_branch", s0done)
     st.label(s0done)
     if fp32scale():
         # every block's S(0) (the blocks without a tile hold zeros: harmless)
-        for b in range(NB):
+        for b in range(nb()):
             for cb in range(4):
                 for ins in scale_ops(b, cb):
                     st.emit(ins)
     st.raw(f"s_mov_b32 {KV0}, 0")
     first_done = w4.newlabel("firstdone")
-    for b in range(NB):
+    for b in range(nb()):
         if b > 0:
             st.raw(f"s_cmp_eq_u32 {TB[b]}, 0")
             st.branch("s_cbranch_scc1", first_done)
@@ -771,13 +815,20 @@ def prologue(st, causal):
         for e in exp_ops(b):
             st.emit(e)
     st.label(first_done)
+    if LATE_V0K1:
+        # V(0), K(1) landed under S(0) and the first softmax: their images
+        # (unread by S(0)) are published by the barrier below
+        st.raw("s_waitcnt vmcnt(0)")
+        for i in range(NPIECE):
+            st.raw(f"ds_write_b128 %[vlds], {VST1(i)} offset:{VBUF[0] + PASSL * i}")
+            st.raw(f"ds_write_b128 %[klds], {KST1(i)} offset:{KBUF[1] + PASSL * i}")
     # every wave's S(0) K reads are done before iteration 0's DMA refills kbuf[0]
     st.lgkm_all()
     st.raw("s_barrier")
     st.raw(f"s_mov_b32 {SJ}, 0")
     # NP of iteration 0: the blocks with a tile
     st.raw(f"s_mov_b32 {SNP}, 0")
-    for b in range(NB):
+    for b in range(nb()):
         st.raw(f"s_cmp_lg_u32 {TB[b]}, 0")
         st.raw(f"s_cselect_b32 {STMP}, 1, 0")
         st.raw(f"s_add_u32 {SNP}, {SNP}, {STMP}")
@@ -843,11 +894,11 @@ def body(st, p, causal, Lb):
     st.label(Lb["loop"][p], drain_lgkm=True)
     st.raw(f"s_add_u32 {SJ1}, {SJ}, 1")
     st.raw(f"s_add_u32 {SJ2}, {SJ}, 2")
-    lbl = {k: w4.newlabel(f"np{k}_") for k in range(1, NB + 1)}
-    for k in range(NB, 1, -1):
+    lbl = {k: w4.newlabel(f"np{k}_") for k in range(1, nb() + 1)}
+    for k in range(nb(), 1, -1):
         st.raw(f"s_cmp_eq_u32 {SNP}, {k}")
         st.branch("s_cbranch_scc1", lbl[k])
-    for k in range(1, NB + 1):
+    for k in range(1, nb() + 1):
         if k > 1:
             st.label(lbl[k])
         st.raw(f"s_cmp_gt_u32 {TB[k - 1]}, {SJ1}")   # block k-1 has tile j+1: steady
@@ -856,7 +907,7 @@ def body(st, p, causal, Lb):
             st.raw(f"s_cmp_eq_u32 {TB[0]}, {SJ1}")   # every block ends at tile j
             st.branch("s_cbranch_scc1", K(k, 0))
         st.branch("s_branch", K(k, k - 1))
-    for np_, nq in KINDS:
+    for np_, nq in kinds():
         st.label(K(np_, nq))
         st.raw(f"s_mov_b32 {SNP}, {nq}")             # NP of iteration j+1
         iteration(st, p, np_, nq, causal, Lb)
@@ -879,7 +930,7 @@ def body(st, p, causal, Lb):
 def generate(causal):
     st = Stream()
     Lb = {k: [w4.newlabel(f"{k}{p}") for p in range(2)]
-          for k in ["loop", "end"] + [f"k_{kname(*x)}" for x in KINDS] + [f"slow_{kname(*x)}" for x in KINDS]}
+          for k in ["loop", "end"] + [f"k_{kname(*x)}" for x in kinds()] + [f"slow_{kname(*x)}" for x in kinds()]}
     Lb["done"] = w4.newlabel("done")
     prologue(st, causal)
     body(st, 0, causal, Lb)
@@ -887,7 +938,7 @@ def generate(causal):
     st.label(Lb["done"], drain_lgkm=True)
     stamp_now(st, 76)
     end = w4.newlabel("epidone")
-    for b in range(NB):
+    for b in range(nb()):
         if b > 0:
             st.raw(f"s_cmp_eq_u32 {TB[b]}, 0")
             st.branch("s_cbranch_scc1", end)
@@ -924,7 +975,7 @@ def cxx(causal, bf16, lines):
     aclob = ", ".join(f'"a{i}"' for i in range(NA))
     sclob = ", ".join(f'"s{i}"' for i in range(NS_LO, NS_DIAG if STAMPS else NS_HI))
     name = (("w4p_item_causal" if causal else "w4p_item_noncausal") + ("_d64" if NT == 2 else "")
-            + ("_bf16" if bf16 else "_f16"))
+            + ("_nb2" if nb() == 2 else "") + ("_bf16" if bf16 else "_f16"))
     blocks = ",\n        ".join(f'[qr{b}] "s"(rn.qr[{b}]), [kvh{b}] "s"(rn.kvh[{b}]), [t{b}] "s"(rn.t[{b}])'
                                  for b in range(NB))
     return f"""
@@ -956,8 +1007,11 @@ def main():
         for bf16 in (False, True):
             set_dtype(bf16)
             for causal in (False, True):
-                w4._lbl[0] = 0
-                text += cxx(causal, bf16, generate(causal))
+                for n in (4, 2):
+                    CURNB["nb"] = n
+                    w4._lbl[0] = 0
+                    text += cxx(causal, bf16, generate(causal))
+                CURNB["nb"] = 4
     set_dtype(False)
     set_hd(128)
     with open(out, "w") as f:
