@@ -233,10 +233,29 @@ def stamp_path_end(st):
         st.raw(f"s_add_u32 s{83 + k}, s{83 + k}, s91")
 
 
+# one-block iterations' LDS read-ahead experiments: W4_XP=p1v8 -- V^T
+# fragments 8 MFMAs ahead instead of 6; p1k2 -- K fragments two 16-key
+# blocks ahead instead of one (the third set in block 1's free S registers)
+P1V8 = "p1v8" in w4.XP
+P1K2 = "p1k2" in w4.XP
+
+
 def vahead(np_):
     """V^T fragments read ahead of their PV MFMAs: >= 8 MFMAs of cover for the
     LDS latency (at head_dim 64 at most the tile's 8)"""
+    if np_ == 1 and P1V8:
+        return min(8, 2 * NE)
     return min({1: 6, 2: 4}.get(np_, 3), 2 * NE)
+
+
+def kreg(cb, t, one=False):
+    """K fragment register of (16-key block cb, k-step t); one (P1K2, one-block
+    kinds): three sets, key block 2's in block 1's S registers v16-v31"""
+    if one and cb == 2:
+        return R("v", 16 + 4 * t, 4)
+    if one and cb == 3:
+        return KF(t)  # key block 0's set, consumed by then
+    return KF(kslot(cb, t))
 
 
 def kslot(cb, t):
@@ -245,9 +264,9 @@ def kslot(cb, t):
     return 4 * (cb & 1) + t if NT == 4 else 2 * cb + t
 
 
-def k_read(t, cb, kb):
-    s = kslot(cb, t)
-    return dsr(f"ds_read_b128 {KF(s)}, {KADDR[t]} offset:{kb + 16 * ROWB * cb}", KF(s), KADDR[t])
+def k_read(t, cb, kb, one=False):
+    r = kreg(cb, t, one)
+    return dsr(f"ds_read_b128 {r}, {KADDR[t]} offset:{kb + 16 * ROWB * cb}", r, KADDR[t])
 
 
 def k_reads_tile(kb):
@@ -264,11 +283,11 @@ def v_reads(f, vb):
             dsr(f"ds_read_b64_tr_b16 {VF(slot, 1)}, {a} offset:{off + 16 * ROWB}", VF(slot, 1), a)]
 
 
-def qk_chain(b, cb):
+def qk_chain(b, cb, one=False):
     out = []
     for t in range(NT):
         c = NEGM(b) if t == 0 else S(b, cb)
-        out.append(mfma(S(b, cb), KF(kslot(cb, t)), Q(b, t), c))
+        out.append(mfma(S(b, cb), kreg(cb, t, one), Q(b, t), c))
     return out
 
 
@@ -345,16 +364,20 @@ def phase_a(st, p, nq, np_):
                 st.emit(r)
         return [], []
     chains = [(b, cb) for cb in range(4) for b in range(nq)]
+    one = P1K2 and nq == 1 and np_ == 1 and NT == 4  # (kind (2, 1): block 1 still converts its P from v16-v31)
     mf = []
     for b, cb in chains:
-        mf += qk_chain(b, cb)
+        mf += qk_chain(b, cb, one)
     n = len(mf)
     gaps = {}
 
     def put(k, ins):
         gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
 
-    put(0, [k_read(t, 0, kb) for t in range(NT)] if NT == 4 else k_reads_tile(kb))
+    if one:
+        put(0, [k_read(t, cb, kb, one) for cb in range(2) for t in range(NT)])
+    else:
+        put(0, [k_read(t, 0, kb) for t in range(NT)] if NT == 4 else k_reads_tile(kb))
     for x, (b, cb) in enumerate(chains):
         c = cvt_block(b, cb)
         if cb == 0:
@@ -362,7 +385,11 @@ def phase_a(st, p, nq, np_):
         else:
             put(NT * x - 1, c[0])
             put(NT * x, c[1])
-        if b == 0 and cb < 3 and NT == 4:
+        if one:
+            if cb < 2:
+                for t in range(NT):
+                    put(NT * x + 1 + t % 3, k_read(t, cb + 2, kb, one))
+        elif b == 0 and cb < 3 and NT == 4:
             for t in range(NT):
                 put(NT * x + 1 + t % 3, k_read(t, cb + 1, kb))
         if x >= lag():
