@@ -399,7 +399,7 @@ constexpr kernel_fn pick_kernel() {
 // W4P: 4 waves x 16 query rows of each of two (G = 1) or four (G = 2) 64-row
 // blocks, K/V double-buffered (64 KB)
 #define FA_CFG_W4PD(ID, G, C, DT, HDIM, NAME)                                          \
-  {{ID, 128 * (G), 64, 4, C, 0, kW4PLdsBytes, NAME, DT, HDIM}, 0, 5 + (G),               \
+  {{ID, 128 * (G), 64, 4, C, 0, w4p_lds_bytes<G, HDIM>(), NAME, DT, HDIM}, 0, 5 + (G),    \
    pick_kernel<4, 64, C, 5 + (G), 0, DT, HDIM>()}
 #define FA_CFG_W4P(ID, G, C, DT, NAME) FA_CFG_W4PD(ID, G, C, DT, 128, NAME)
 

@@ -127,7 +127,7 @@ KOFF = ["%[koff]"] + [R("v", 208 + i) for i in range(3)]
 VOFF = ["%[voff]"] + [R("v", 211 + i) for i in range(3)]
 EPI = [f"v{144 + i}" for i in range(8)]       # epilogue staging (the free V^T slots)
 XY = ["v152", "v153", "v154", "v155"]         # one store: X = v152,153 ; Y = v154,155
-NV = 214
+NV = 217   # v214-v216: the V image bases + 64 KiB (dbl programs)
 
 
 def O(b, e, i=None):       # O^T accumulator, block b, d-block e
@@ -156,6 +156,44 @@ NA = 240
 # LDS images (W4's): K at 0 / 16384, V at 32768 / 49152
 KBUF = [0, 16384]
 VBUF = [32768, 49152]
+
+
+# Two key tiles per barrier (the pair program at head_dim 128, as
+# gen_w4_item.py's dbl): four K / V images (K at 0-48 KiB, V at 64-112 KiB),
+# tiles DMA'd two ahead, a pair iteration of two steady tiles -- same
+# kind, every live block steady for both: T[k-1] >= j + 4 -- with one DMA
+# wait and one barrier, the second tile's key-block-0 fragments read in the
+# first tile's PV tail.  W4_XP=nodblp: the one-tile loop.
+def pdbl():
+    return nb() == 2 and NT == 4 and "nodblp" not in w4.XP and "p1nolds" not in w4.XP
+
+
+def nbuf():
+    return 4 if pdbl() else 2
+
+
+def look():
+    return 2 if pdbl() else 1
+
+
+def kbuf(i):  # ds offset of tile i's K image
+    return 16384 * (i % nbuf())
+
+
+def vbuf(i):  # ds offset of tile i's V image from vaddr()
+    return 16384 * (i % 4) if pdbl() else VBUF[i % 2]
+
+
+def vbuf_abs(i):  # LDS offset of tile i's V image (M0 of its DMA)
+    return 65536 + 16384 * (i % 4) if pdbl() else VBUF[i % 2]
+
+
+def vaddr(k):
+    return ("v214", "v215")[k] if pdbl() else VADDR[k]
+
+
+def vlds():
+    return "v216" if pdbl() else "%[vlds]"
 KADDR = [f"%[ka{t}]" for t in range(4)]
 VADDR = ["%[va0]", "%[va1]"]
 
@@ -278,7 +316,7 @@ def v_reads(f, vb):
     u, e = divmod(f, NE)
     slot = f % 8
     off = vb + 32 * ROWB * u + 512 * (e >> 1)
-    a = VADDR[e & 1]
+    a = vaddr(e & 1)
     return [dsr(f"ds_read_b64_tr_b16 {VF(slot, 0)}, {a} offset:{off}", VF(slot, 0), a),
             dsr(f"ds_read_b64_tr_b16 {VF(slot, 1)}, {a} offset:{off + 16 * ROWB}", VF(slot, 1), a)]
 
@@ -326,14 +364,15 @@ def pv_mfmas(np_):
 
 
 def dma_pieces(p):
-    """LDS-DMA of K(j+2) -> kbuf[p], V(j+1) -> vbuf[1-p]: (M0 set, load)
+    """LDS-DMA of K(j+1+look) -> its K image, V(j+look) -> its V image
+    (one tile ahead: K(j+2) -> kbuf[p], V(j+1) -> vbuf[1-p]): (M0 set, load)
     pairs, then the descriptors advance one tile (gen_w4_item.dma_loads)"""
     pairs = []
     for i in range(NPIECE):
-        pairs.append((salu(f"s_add_u32 m0, %[dmab], {KBUF[p] + 1024 * i}"),
+        pairs.append((salu(f"s_add_u32 m0, %[dmab], {kbuf(p + 1 + look()) + 1024 * i}"),
                       vmem(f"buffer_load_dwordx4 {KD(i)}, {SK}, 0 offen lds", r=[KD(i)])))
     for i in range(NPIECE):
-        pairs.append((salu(f"s_add_u32 m0, %[dmab], {VBUF[1 - p] + 1024 * i}"),
+        pairs.append((salu(f"s_add_u32 m0, %[dmab], {vbuf_abs(p + look()) + 1024 * i}"),
                       vmem(f"buffer_load_dwordx4 {VD(i)}, {SV}, 0 offen lds", r=[VD(i)])))
     tb = hex(TILEB)
     adv = [[salu(f"s_add_u32 s40, s40, {tb}"), salu("s_addc_u32 s41, s41, 0")],
@@ -346,13 +385,13 @@ def dma_pieces(p):
 # ---------------------------------------------------------------------------
 # one iteration: phase A / mask / phase B
 # ---------------------------------------------------------------------------
-def phase_a(st, p, nq, np_):
+def phase_a(st, p, nq, np_, k0_issued=False):
     """QK^T(j+1) of blocks 0..nq-1 from kbuf[1-p] beside the fp16 conversion of
     P(j) of blocks 0..np-1 (each just before the chain that overwrites its
     scores), the running maxima of S(j+1), the K reads, the stage's LDS-DMA
     and the first V^T fragments of PV(j).  nq = 0 (the last tile): the
     conversions and V^T reads alone."""
-    kb = KBUF[1 - p]
+    kb = kbuf(p + 1)
     va = vahead(np_)
     if nq == 0:
         for b in range(np_):
@@ -360,7 +399,7 @@ def phase_a(st, p, nq, np_):
                 for c in cvt_block(b, cb):
                     st.emit(c)
         for f in range(va):
-            for r in v_reads(f, VBUF[p]):
+            for r in v_reads(f, vbuf(p)):
                 st.emit(r)
         return [], []
     chains = [(b, cb) for cb in range(4) for b in range(nq)]
@@ -374,7 +413,12 @@ def phase_a(st, p, nq, np_):
     def put(k, ins):
         gaps.setdefault(k, []).extend(ins if isinstance(ins, list) else [ins])
 
-    if one:
+    if k0_issued:
+        # key block 0's fragments were read in the previous phase B's tail
+        # (pdbl: no barrier between); with P1K2 key block 1's follow now
+        if one:
+            put(0, [k_read(t, 1, kb, one) for t in range(NT)])
+    elif one:
         put(0, [k_read(t, cb, kb, one) for cb in range(2) for t in range(NT)])
     else:
         put(0, [k_read(t, 0, kb) for t in range(NT)] if NT == 4 else k_reads_tile(kb))
@@ -424,7 +468,7 @@ def phase_a(st, p, nq, np_):
         put(min(g + i, n), ins)
     # the first V^T fragments of PV(j) (V(j) is ready since the last barrier)
     for f in range(va):
-        for i, r in enumerate(v_reads(f, VBUF[p])):
+        for i, r in enumerate(v_reads(f, vbuf(p))):
             put(min(max(0, n - 2 * va) + 2 * f + i, n), r)
     if fp32scale():
         for y in range(max(0, len(chains) - lag()), len(chains)):
@@ -461,11 +505,11 @@ def mask_pass(st, nq, causal):
     st.label(done)
 
 
-def phase_b(st, p, nq, np_, leftover, label_slow, label_end, late=()):
+def phase_b(st, p, nq, np_, leftover, label_slow, label_end, late=(), kpre=None):
     """PV(j) of blocks 0..np-1 from vbuf[p]; the rescale decision over the
     blocks 0..nq-1 at DEC_GAP, exp2 of their S(j+1) after it.  nq = 0: the
     PV alone."""
-    vb = VBUF[p]
+    vb = vbuf(p)
     mf, frag_first = pv_mfmas(np_)
     n = len(mf)
     gaps = {}
@@ -482,6 +526,12 @@ def phase_b(st, p, nq, np_, leftover, label_slow, label_end, late=()):
         r = v_reads(f, vb)
         put(k + 1, r[0])
         put(k + 2, r[1])
+    if kpre is not None:
+        # pdbl: the next phase A's key-block-0 K fragments (their image was
+        # published by the barrier that opened this pair; the slots' last
+        # reader was this iteration's QK^T)
+        for t in range(NT):
+            put(max(DEC_GAP + 1, n - 2 * NT - 2) + 2 * t, k_read(t, 0, kbuf(kpre)))
     # (head_dim 64: three chains' maxima, two per gap)
     lo = [LEFT_OFF + (i if NT == 4 else i // 2) for i in range(len(leftover))]
     for k, ins in zip(lo, leftover):
@@ -738,6 +788,10 @@ def prologue(st, causal):
             st.raw(f"s_mov_b32 s{r}, 0")
         stamp_now(st, 76)
     st.raw(f"s_mov_b32 {SM0}, m0")
+    if pdbl():
+        st.raw("v_add_u32 v214, 0x10000, %[va0]")
+        st.raw("v_add_u32 v215, 0x10000, %[va1]")
+        st.raw("v_add_u32 v216, 0x10000, %[vlds]")
     st.raw(f"v_mov_b32 {KD(0)}, %[kdma]")
     st.raw(f"v_mov_b32 {VD(0)}, %[vdma]")
     # DMA piece i's sources (gen_w4_item.dma_setup: head_dim 128 / 64)
@@ -803,8 +857,23 @@ def prologue(st, causal):
     if not LATE_V0K1:
         st.raw("s_waitcnt vmcnt(0)")
         for i in range(NPIECE):
-            st.raw(f"ds_write_b128 %[vlds], {VST1(i)} offset:{VBUF[0] + PASSL * i}")
+            st.raw(f"ds_write_b128 {vlds()}, {VST1(i)} offset:{vbuf(0) + PASSL * i}")
             st.raw(f"ds_write_b128 %[klds], {KST1(i)} offset:{KBUF[1] + PASSL * i}")
+    if pdbl():
+        # two tiles ahead: K(2), V(1) by LDS-DMA now (iteration 0's end waits)
+        for i in range(NPIECE):
+            st.raw(f"s_add_u32 m0, %[dmab], {kbuf(2) + 1024 * i}")
+            st.nop(1)
+            st.raw(f"buffer_load_dwordx4 {KD(i)}, {SK}, 0 offen lds")
+        for i in range(NPIECE):
+            st.raw(f"s_add_u32 m0, %[dmab], {vbuf_abs(1) + 1024 * i}")
+            st.nop(1)
+            st.raw(f"buffer_load_dwordx4 {VD(i)}, {SV}, 0 offen lds")
+        tb = hex(TILEB)
+        for ins in (f"s_add_u32 s40, s40, {tb}", "s_addc_u32 s41, s41, 0", f"s_sub_i32 {SKREM}, {SKREM}, {tb}",
+                    f"s_max_i32 s42, {SKREM}, 0", f"s_add_u32 s44, s44, {tb}", "s_addc_u32 s45, s45, 0",
+                    f"s_sub_i32 {SVREM}, {SVREM}, {tb}", f"s_max_i32 s46, {SVREM}, 0"):
+            st.raw(ins)
     st.raw("s_waitcnt lgkmcnt(0)")
     st.raw("s_barrier")
     st.nop(2)
@@ -847,7 +916,7 @@ def prologue(st, causal):
         # (unread by S(0)) are published by the barrier below
         st.raw("s_waitcnt vmcnt(0)")
         for i in range(NPIECE):
-            st.raw(f"ds_write_b128 %[vlds], {VST1(i)} offset:{VBUF[0] + PASSL * i}")
+            st.raw(f"ds_write_b128 {vlds()}, {VST1(i)} offset:{vbuf(0) + PASSL * i}")
             st.raw(f"ds_write_b128 %[klds], {KST1(i)} offset:{KBUF[1] + PASSL * i}")
     # every wave's S(0) K reads are done before iteration 0's DMA refills kbuf[0]
     st.lgkm_all()
@@ -912,6 +981,32 @@ def epilogue_block(st, b):
 
 
 # ---------------------------------------------------------------------------
+def double_iter(st, p, k, causal, Lb):
+    """pdbl: steady tiles j, j+1 (j mod 4 = p) of kind (k, k), one barrier"""
+    q = (p + 1) % nbuf()
+    stamp_path(st, NB - k)
+    left, late = phase_a(st, p, k, k)
+    mid = Lb[f"dmid{k}"][p]
+    phase_b(st, p, k, k, left, Lb[f"dslow1_{k}"][p], mid, late, kpre=p + 2)
+    st.label(mid)
+    left, late = phase_a(st, q, k, k, k0_issued=True)
+    phase_b(st, q, k, k, left, Lb[f"dslow2_{k}"][p], Lb[f"dend{k}"][p], late)
+    st.label(Lb[f"dend{k}"][p], drain_lgkm=True)
+    stamp_path_end(st)
+    if STAMPS:  # two tiles: count the path twice
+        st.raw(f"s_add_u32 s{83 + NB - k}, s{83 + NB - k}, 1")
+    st.raw("s_waitcnt vmcnt(0)")
+    st.raw("s_barrier")
+    if STAMPS:
+        stamp_now(st, 72)
+        st.raw("s_sub_u32 s75, s72, s76")
+        st.raw("s_add_u32 s88, s88, s75")
+    st.raw(f"s_add_u32 {SJ}, {SJ}, 2")
+    st.raw(f"s_cmp_lt_u32 {SJ}, {TB[0]}")
+    st.far("s_cbranch_scc1", Lb["loop"][(p + 2) % nbuf()])
+    st.far("s_branch", Lb["done"])
+
+
 def body(st, p, causal, Lb):
     """iteration j (parity p = j & 1): the kind of (NP, NQ) = (#{T_b > j},
     #{T_b > j+1}) -- NP carried from the previous iteration's NQ, NQ = NP
@@ -921,6 +1016,21 @@ def body(st, p, causal, Lb):
     st.label(Lb["loop"][p], drain_lgkm=True)
     st.raw(f"s_add_u32 {SJ1}, {SJ}, 1")
     st.raw(f"s_add_u32 {SJ2}, {SJ}, 2")
+    if pdbl() and p % 2 == 1:
+        # kind (k, k) twice: T[k-1] >= j + 4 (every live block has tiles
+        # j+1 and j+2, neither its last: no mask, no drain) -- the block
+        # tile counts are the workgroup's, so every wave takes the same path
+        single = w4.newlabel("single")
+        st.raw(f"s_add_u32 {STMP}, {SJ}, 3")
+        for k in range(1, nb() + 1):
+            nxt = w4.newlabel("dnext")
+            st.raw(f"s_cmp_eq_u32 {SNP}, {k}")
+            st.branch("s_cbranch_scc0", nxt)
+            st.raw(f"s_cmp_lt_u32 {STMP}, {TB[k - 1]}")
+            st.branch("s_cbranch_scc0", single)
+            double_iter(st, p, k, causal, Lb)
+            st.label(nxt)
+        st.label(single)
     lbl = {k: w4.newlabel(f"np{k}_") for k in range(1, nb() + 1)}
     for k in range(nb(), 1, -1):
         st.raw(f"s_cmp_eq_u32 {SNP}, {k}")
@@ -948,20 +1058,22 @@ def body(st, p, causal, Lb):
         st.raw("s_add_u32 s88, s88, s75")
     st.raw(f"s_add_u32 {SJ}, {SJ}, 1")
     st.raw(f"s_cmp_lt_u32 {SJ}, {TB[0]}")
-    if p == 0:
-        st.branch("s_cbranch_scc0", Lb["done"])
+    jump = st.far if pdbl() else st.branch
+    if p < nbuf() - 1:
+        jump("s_cbranch_scc0", Lb["done"])  # else on to body p + 1
     else:
-        st.branch("s_cbranch_scc1", Lb["loop"][0])
+        jump("s_cbranch_scc1", Lb["loop"][0])
 
 
 def generate(causal):
     st = Stream()
-    Lb = {k: [w4.newlabel(f"{k}{p}") for p in range(2)]
-          for k in ["loop", "end"] + [f"k_{kname(*x)}" for x in kinds()] + [f"slow_{kname(*x)}" for x in kinds()]}
+    dl = [f"{d}{k}" for k in range(1, nb() + 1) for d in ("dmid", "dend", "dslow1_", "dslow2_")]
+    Lb = {k: [w4.newlabel(f"{k}{p}") for p in range(nbuf())]
+          for k in ["loop", "end"] + [f"k_{kname(*x)}" for x in kinds()] + [f"slow_{kname(*x)}" for x in kinds()] + dl}
     Lb["done"] = w4.newlabel("done")
     prologue(st, causal)
-    body(st, 0, causal, Lb)
-    body(st, 1, causal, Lb)
+    for p in range(nbuf()):
+        body(st, p, causal, Lb)
     st.label(Lb["done"], drain_lgkm=True)
     stamp_now(st, 76)
     end = w4.newlabel("epidone")
@@ -996,6 +1108,16 @@ HEADER = """// GENERATED by gen_w4p_item.py -- do not edit.
 """
 
 
+def header():
+    # the head_dim-128 pair programs' LDS layout (fa_w4p_kernel.hpp): 1 = four
+    # K / V images per tensor (two key tiles per barrier), 128 KiB
+    CURNB["nb"] = 2
+    set_hd(128)
+    on = pdbl()
+    CURNB["nb"] = 4
+    return HEADER + f"#define FA_W4P_DBL {1 if on else 0}\n"
+
+
 def cxx(causal, bf16, lines):
     body_ = "\n".join(f'      "{ln}\\n"' for ln in lines)
     vclob = ", ".join(f'"v{i}"' for i in range(NV))
@@ -1028,7 +1150,7 @@ __device__ __forceinline__ void {name}(const W4PRun& rn, const W4Lane& ln) {{
 
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else "fa_w4p_item.inc"
-    text = HEADER
+    text = header()
     for hd in (128, 64):
         set_hd(hd)
         for bf16 in (False, True):

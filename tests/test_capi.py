@@ -86,8 +86,8 @@ def test_config_table():
         # K and V image buffers of 256-B row slots: double-buffered, or three
         # rotating buffers each for the LDS-DMA configs
         nbuf = 3 if "_dma_" in c.name else 2
-        if "_asm_persistent_" in c.name and c.head_dim == 128:
-            nbuf = 4  # the W4 program's two key tiles per barrier (gen_w4_item.py dbl)
+        if ("_asm_persistent_" in c.name or "_asm_pair_" in c.name) and c.head_dim == 128:
+            nbuf = 4  # the W4 / W4P pair programs' two key tiles per barrier (gen_w4*_item.py)
         need = 2 * nbuf * c.block_n * 256
         if "_pingpong_persistent_" in c.name and "_dma_" not in c.name and not c.causal:
             need = max(need, KVPAIR_LDS)  # room for the KV-pair tail halves
