@@ -271,11 +271,15 @@ def stamp_path_end(st):
         st.raw(f"s_add_u32 s{83 + k}, s{83 + k}, s91")
 
 
-# one-block iterations' LDS read-ahead experiments: W4_XP=p1v8 -- V^T
-# fragments 8 MFMAs ahead instead of 6; p1k2 -- K fragments two 16-key
-# blocks ahead instead of one (the third set in block 1's free S registers)
-P1V8 = "p1v8" in w4.XP
-P1K2 = "p1k2" in w4.XP
+# one-block iterations' LDS read-ahead: V^T fragments 8 MFMAs ahead instead
+# of 6 (W4_XP=nop1v8: 6), K fragments two 16-key blocks ahead instead of one
+# (the third set in block 1's free S registers; W4_XP=nop1k2: one).  Measured
+# alone on the one-tile-per-barrier program: +0.8 / -0.4 %; together on the
+# two-tiles-per-barrier program: config 1 +1.9 %, B=2 H=8 S=2048 causal
+# +1.4 %, +0.4-0.5 % on S=512 causal / H=8 S=4096 causal / H=16 S=2048
+# (bit-identical; profiles/r06_ab_w4p_probes.jsonl)
+P1V8 = "nop1v8" not in w4.XP
+P1K2 = "nop1k2" not in w4.XP
 
 
 def vahead(np_):
@@ -451,6 +455,8 @@ def phase_a(st, p, nq, np_, k0_issued=False):
     # state); two or more blocks spread them over two gaps each, one shares gaps
     pairs, adv = dma_pieces(p)
     late = []
+    if nq == 1 and np_ == 1 and "p1nodma" in w4.XP:
+        pairs, adv = [], []   # timing-only probe: no K/V DMA in one-block iterations
     if nq == 1 and np_ == 1 and "p1dmaa" not in w4.XP:
         # one-block iterations: the V tile's pieces and descriptor advance in
         # phase B (its buffer is free for the whole iteration) -- eight pieces
@@ -551,6 +557,8 @@ def phase_b(st, p, nq, np_, leftover, label_slow, label_end, late=(), kpre=None)
             dec.append(valu(f"v_max_f32 {T[0]}, {T[0]}, {RMAX[3]}", r=[T[0], RMAX[3]], w=[T[0]]))
     dec.append(valu(f"v_cmp_lt_f32 vcc, {RESCALE}, {m}", r=[m]))
     exs = [e for b in range(nq) for e in exp_ops(b)]
+    if nq == 1 and np_ == 1 and "p1noexp" in w4.XP:
+        exs = []   # timing-only probe: no exp2 in one-block iterations
     n_g = n - DEC_GAP
     for i, e in enumerate(exs):
         put(DEC_GAP + 1 + (i * n_g) // len(exs), e)
