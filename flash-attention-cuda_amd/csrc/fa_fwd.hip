@@ -344,7 +344,8 @@ struct Config {
   int kind;   // 0 = one workgroup per item, 1 = split-KV, 2 = persistent, 3 = KV-pair,
               // 4 = KV-quad, 5 = persistent, one wave per SIMD (W4, asm item program),
               // 6 = paired 64-row query blocks, one wave per SIMD (W4P, asm item program),
-              // 7 = two pairs per workgroup (the same program)
+              // 7 = two pairs per workgroup (the same program), 8 = one 64-row
+              // block per workgroup (the same program)
   kernel_fn fn;
 };
 
@@ -356,6 +357,8 @@ constexpr kernel_fn pick_kernel() {
     return fa_fwd_w4p_kernel<(C != 0), DT == 1, 1, HDIM>;
   else if constexpr (KIND == 7)
     return fa_fwd_w4p_kernel<(C != 0), DT == 1, 2, HDIM>;
+  else if constexpr (KIND == 8)
+    return fa_fwd_w4p_kernel<(C != 0), DT == 1, 0, HDIM>;
 
   else if constexpr (KIND == 3)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
@@ -402,6 +405,10 @@ constexpr kernel_fn pick_kernel() {
   {{ID, 128 * (G), 64, 4, C, 0, w4p_lds_bytes<G, HDIM>(), NAME, DT, HDIM}, 0, 5 + (G),    \
    pick_kernel<4, 64, C, 5 + (G), 0, DT, HDIM>()}
 #define FA_CFG_W4P(ID, G, C, DT, NAME) FA_CFG_W4PD(ID, G, C, DT, 128, NAME)
+// W4P singles: 4 waves x 16 query rows of one 64-row block
+#define FA_CFG_W4PS(ID, C, DT, HDIM, NAME)                                             \
+  {{ID, 64, 64, 4, C, 0, w4p_lds_bytes<0, HDIM>(), NAME, DT, HDIM}, 0, 8,                 \
+   pick_kernel<4, 64, C, 8, 0, DT, HDIM>()}
 
 // Only tiers the dispatcher picks, explicit entry points (split-KV) and the
 // baselines a test compares against (the per-item ping-pong 2/3: the
@@ -482,6 +489,16 @@ static const Config kConfigs[] = {
     FA_CFG_W4PD(61, 2, 1, 0, 64, "d64_bm256_bn64_w4x64_m16_asm_quad_causal"),
     FA_CFG_W4PD(62, 2, 0, 1, 64, "bf16_d64_bm256_bn64_w4x64_m16_asm_quad_noncausal"),
     FA_CFG_W4PD(63, 2, 1, 1, 64, "bf16_d64_bm256_bn64_w4x64_m16_asm_quad_causal"),
+    // one 64-row block per workgroup on the pair program (launches of at most
+    // one block per CU)
+    FA_CFG_W4PS(64, 0, 0, 128, "bm64_bn64_w4x16_m16_asm_single_noncausal"),
+    FA_CFG_W4PS(65, 1, 0, 128, "bm64_bn64_w4x16_m16_asm_single_causal"),
+    FA_CFG_W4PS(66, 0, 1, 128, "bf16_bm64_bn64_w4x16_m16_asm_single_noncausal"),
+    FA_CFG_W4PS(67, 1, 1, 128, "bf16_bm64_bn64_w4x16_m16_asm_single_causal"),
+    FA_CFG_W4PS(68, 0, 0, 64, "d64_bm64_bn64_w4x16_m16_asm_single_noncausal"),
+    FA_CFG_W4PS(69, 1, 0, 64, "d64_bm64_bn64_w4x16_m16_asm_single_causal"),
+    FA_CFG_W4PS(70, 0, 1, 64, "bf16_d64_bm64_bn64_w4x16_m16_asm_single_noncausal"),
+    FA_CFG_W4PS(71, 1, 1, 64, "bf16_d64_bm64_bn64_w4x16_m16_asm_single_causal"),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -675,6 +692,19 @@ static int select_tier(int batch, int heads, int seq_len, int causal, bool pair)
   const long long wg64 = bh * ((seq_len + 63) / 64);
   const long long nqb256 = (seq_len + 255) / 256;
   const int c = causal ? 1 : 0;
+  // at most one 64-row query block per CU (heads of <= 64 blocks): one block
+  // per workgroup on the W4P pair program (singles) -- a pair's second block
+  // adds its prologue Q rows, its iterations and its epilogue to the
+  // workgroup with CUs to spare.  Same process against the tier it replaced
+  // (profiles/r06_ab_w4p_single.jsonl): B=1 H=32 S=512 causal 248 vs pairs
+  // 219, non-causal 474 vs KV-quad 369; S=256 causal 83 vs the 4-wave loop 53,
+  // non-causal 164 vs 114; S=128 22 vs 18 / 44 vs 39, B=4 87 vs 69 / 177 vs
+  // 151; H=16 S=1024 causal 339 vs 312, non-causal 640 vs 535; H=8 S=2048 422
+  // vs 401 / 770 vs 677; H=4 S=4096 487 vs 471 / 751 vs 748; past one block
+  // per CU it loses (H=32 S=768 causal 361 vs 379).  Head_dim 64 non-causal
+  // (pair = false) up to 16 blocks per head: S=512 308 vs KV-quad 276, H=16
+  // S=1024 417 vs 406; H=8 S=2048 507 vs 525, H=4 S=4096 485 vs 607
+  if (wg64 <= num_cus() && (seq_len + 63) / 64 <= (pair ? 64 : 16)) return cfg_for(64, 4, 64, c, 0, 8);
   if (seq_len <= 128) return cfg_for(128, 4, 64, c, 0, 0);
   // causal with about one 256-row item per CU: the snake cannot balance item
   // costs 1..nqb256, so the KV-pair's halved heaviest key loop wins from

@@ -82,11 +82,11 @@ def test_config_table():
             assert c.lds_bytes == 4 * 2 * c.block_n * 256
             continue
         # 64 query rows per wave (one wave per SIMD) or 32
-        assert c.block_m == (64 if "_w4x64_" in c.name else 32) * c.waves
+        assert c.block_m == (64 if "_w4x64_" in c.name else 16 if "_w4x16_" in c.name else 32) * c.waves
         # K and V image buffers of 256-B row slots: double-buffered, or three
         # rotating buffers each for the LDS-DMA configs
         nbuf = 3 if "_dma_" in c.name else 2
-        if ("_asm_persistent_" in c.name or "_asm_pair_" in c.name) and c.head_dim == 128:
+        if any(t in c.name for t in ("_asm_persistent_", "_asm_pair_", "_asm_single_")) and c.head_dim == 128:
             nbuf = 4  # the W4 / W4P pair programs' two key tiles per barrier (gen_w4*_item.py)
         need = 2 * nbuf * c.block_n * 256
         if "_pingpong_persistent_" in c.name and "_dma_" not in c.name and not c.causal:
@@ -115,10 +115,14 @@ def test_select_config(causal):
     assert "_persistent_" in cfgs[fa.select_config(1, 32, 8192, causal)].name
     # causal launches of <= 2 rounds of pairs up to S=2048: the paired tier;
     # non-causal ones of <= 256 64-row blocks under 3/4 of a round: the KV-quad
-    short = "_asm_pair_" if causal else "_kvquad_"
-    assert short in cfgs[fa.select_config(1, 8, 2048, causal)].name
-    assert short in cfgs[fa.select_config(1, 32, 512, causal)].name
-    assert "_w4_" in cfgs[fa.select_config(1, 32, 256, causal)].name
+    # launches of <= 1 64-row block per CU (heads of <= 64 blocks): one block
+    # per workgroup on the paired tier's program
+    for b, h, s in ((1, 8, 2048), (1, 32, 512), (1, 32, 256), (1, 4, 4096), (1, 64, 256), (1, 32, 128),
+                    (4, 32, 128), (1, 1, 1)):
+        assert "_asm_single_" in cfgs[fa.select_config(b, h, s, causal)].name, (b, h, s, causal)
+    assert "_w4_" in cfgs[fa.select_config(8, 32, 128, causal)].name
+    assert "_asm_single_" not in cfgs[fa.select_config(1, 4, 8192, causal)].name  # 128 blocks per head
+    assert "_asm_pair_" in cfgs[fa.select_config(1, 16, 2048, causal)].name  # 512 blocks
     # between the KV-quad's and the paired tier's non-causal shapes: the KV-pair
     assert "_kvpair_" in cfgs[fa.select_config(1, 20, 1024, False)].name
     # long heads, few of them: causal -> the KV-quad's four-way key split

@@ -1,5 +1,6 @@
 """Multi-block short-sequence tier (bm128_bn64_w4x32_m16_asm_pair_*: two 64-row
-query blocks per workgroup, bm256_bn64_w4x64_m16_asm_quad_*: four;
+query blocks per workgroup, bm256_bn64_w4x64_m16_asm_quad_*: four,
+bm64_bn64_w4x16_m16_asm_single_*: one, on the pair program;
 fa_w4p_kernel.hpp + the generated item program fa_w4p_item.inc).
 
 A workgroup holds two or four 64-row query blocks of one head (causal: pairs
@@ -23,6 +24,7 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-3
 PAIR = "bm128_bn64_w4x32_m16_asm_pair"
 QUAD = "bm256_bn64_w4x64_m16_asm_quad"
+SINGLE = "bm64_bn64_w4x16_m16_asm_single"
 
 
 def _fa():
@@ -99,17 +101,18 @@ SHAPES = [
 ]
 
 
-TIERS = [PAIR, QUAD]
+TIERS = [PAIR, QUAD, SINGLE]
+TIER_IDS = ["pair", "quad", "single"]
 
 
-@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
+@pytest.mark.parametrize("tier", TIERS, ids=TIER_IDS)
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
 def test_pair_matches_oracle(shape, causal, tier):
     _check(*shape, causal, seed=700, tier=tier)
 
 
-@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
+@pytest.mark.parametrize("tier", TIERS, ids=TIER_IDS)
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("s", [256, 1000, 2048])
 def test_pair_peaked_rescale(s, causal, tier):
@@ -123,14 +126,14 @@ def _random_shapes(n, seed):
             for _ in range(n)]
 
 
-@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
+@pytest.mark.parametrize("tier", TIERS, ids=TIER_IDS)
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("shape", _random_shapes(6, 2027), ids=lambda s: "x".join(map(str, s)))
 def test_pair_random_shapes(shape, causal, tier):
     _check(*shape, causal, seed=720, tier=tier)
 
 
-@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
+@pytest.mark.parametrize("tier", TIERS, ids=TIER_IDS)
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("shape", [(1, 32, 1024), (1, 8, 1000), (2, 3, 320)], ids=lambda s: "x".join(map(str, s)))
 def test_pair_bf16(shape, causal, tier):
@@ -180,7 +183,7 @@ def test_pair_causal_row0_and_ones():
         assert torch.equal(o1, ones)
 
 
-@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
+@pytest.mark.parametrize("tier", TIERS, ids=TIER_IDS)
 def test_pair_deterministic(tier):
     fa = _fa()
     q, k, v = (_rand((1, 32, 1024, 128), 750 + i) for i in range(3))
@@ -211,25 +214,55 @@ D64_SHAPES = [(1, 32, 1024), (1, 8, 1000), (2, 3, 320), (1, 4, 64), (1, 2, 65), 
               (1, 16, 2048), (3, 40, 777), (4, 32, 512)]
 
 
-@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
+@pytest.mark.parametrize("tier", TIERS, ids=TIER_IDS)
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("shape", D64_SHAPES, ids=lambda s: "x".join(map(str, s)))
 def test_pair_d64_matches_oracle(shape, causal, tier):
     _check(*shape, causal, seed=800, tier=tier, d=64)
 
 
-@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
+@pytest.mark.parametrize("tier", TIERS, ids=TIER_IDS)
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("s", [256, 1000, 2048])
 def test_pair_d64_peaked_rescale(s, causal, tier):
     _check(1, 8, s, causal, seed=810, scale=4.0, tier=tier, d=64)
 
 
-@pytest.mark.parametrize("tier", TIERS, ids=["pair", "quad"])
+@pytest.mark.parametrize("tier", TIERS, ids=TIER_IDS)
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("shape", [(1, 32, 1024), (1, 8, 1000), (2, 3, 320)], ids=lambda s: "x".join(map(str, s)))
 def test_pair_d64_bf16(shape, causal, tier):
     _check(*shape, causal, seed=830, dtype=torch.bfloat16, tier=tier, d=64)
+
+
+@pytest.mark.parametrize("d", [128, 64])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["fp16", "bf16"])
+@pytest.mark.parametrize("causal", [False, True])
+def test_single_matches_pair_bitwise(causal, dtype, d):
+    """one block per workgroup runs the pair program with block 1 absent: every
+    block's arithmetic is the pair grouping's (the rescale test per 16-row
+    block), so the outputs are bit-identical"""
+    fa = _fa()
+    pre = ("bf16_" if dtype == torch.bfloat16 else "") + ("d64_" if d == 64 else "")
+    for b, h, s in ((1, 32, 512), (2, 3, 1000), (1, 5, 513), (1, 2, 64)):
+        q, k, v = (_rand((b, h, s, d), 880 + i, 4.0 if i < 2 else 1.0, dtype) for i in range(3))
+        a = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(pre + SINGLE)[causal])
+        p = fa.flash_attention_fwd(q, k, v, causal=causal, config=_ids(pre + PAIR)[causal])
+        assert torch.equal(a, p), (b, h, s)
+
+
+@pytest.mark.parametrize("b,h,s", [(1, 32, 512), (1, 32, 256), (1, 16, 1024), (1, 8, 2048), (1, 4, 4096),
+                                   (2, 16, 512), (1, 64, 256), (4, 32, 128), (1, 3, 1), (2, 5, 100)])
+def test_single_dispatched(b, h, s):
+    """launches of at most one 64-row block per CU (heads of <= 64 blocks) run
+    the single grouping, both masks: against fp32 torch on every head"""
+    fa = _fa()
+    for causal in (False, True):
+        assert "_asm_single_" in fa.configs()[fa.select_config(b, h, s, causal)].name, (b, h, s, causal)
+        q, k, v = (_rand((b, h, s, 128), 890 + i) for i in range(3))
+        out = fa.flash_attention_fwd(q, k, v, causal=causal)
+        torch.cuda.synchronize()
+        assert (out.float() - _torch_ref(q, k, v, causal)).abs().max().item() <= TOL
 
 
 def test_pair_d64_row0_ones_deterministic():
