@@ -49,7 +49,7 @@ SHAPES = [  # (label, batch, heads, seq, causal[, forced tier name | "auto"])
     ("headline_b64_s4096_causal", 64, 32, 4096, True),
     ("s256_b16_noncausal", 16, 32, 256, False),
     # the causal split tier (workspace entry; the default Python path)
-    ("split_h8_s4096_causal", 1, 8, 4096, True, "auto"),
+    ("h8_s4096_causal", 1, 8, 4096, True, "auto"),
     ("split_h4_s8192_causal", 1, 4, 8192, True, "auto"),
     # non-dispatched tile configs (BM, BN, waves) on the same shapes: the
     # 8-wave persistent ping-pong W4 replaced, BN=128 (the reference's long
@@ -61,6 +61,9 @@ SHAPES = [  # (label, batch, heads, seq, causal[, forced tier name | "auto"])
     ("bn128_s8192_noncausal", 1, 32, 8192, False, "bm128_bn128_w4_m16_noncausal"),
     ("bn128_s8192_causal", 1, 32, 8192, True, "bm128_bn128_w4_m16_causal"),
     ("pingpong_item_s8192_causal", 1, 32, 8192, True, "bm256_bn64_w8_m16_pingpong_causal"),
+    # what the round-6 singles replaced at S=512 (the pair grouping, the KV-quad)
+    ("pair_s512_causal", 1, 32, 512, True, "bm128_bn64_w4x32_m16_asm_pair_causal"),
+    ("kvquad_cfg0_s512_noncausal", 1, 32, 512, False, "bm64_bn64_w8_m16_kvquad_noncausal"),
     # the KV-pair the round-5 paired / quad tier replaced on short causal launches
     ("kvpair_cfg1_s1024_causal", 1, 32, 1024, True, "bm128_bn64_w8_m16_kvpair_causal"),
     ("kvpair_s2048_causal", 1, 32, 2048, True, "bm128_bn64_w8_m16_kvpair_causal"),
