@@ -345,7 +345,8 @@ struct Config {
               // 4 = KV-quad, 5 = persistent, one wave per SIMD (W4, asm item program),
               // 6 = paired 64-row query blocks, one wave per SIMD (W4P, asm item program),
               // 7 = two pairs per workgroup (the same program), 8 = one 64-row
-              // block per workgroup (the same program)
+              // block per workgroup (the same program), 9 = causal singles
+              // and pairs mixed to fill the CUs (the same program)
   kernel_fn fn;
 };
 
@@ -359,6 +360,8 @@ constexpr kernel_fn pick_kernel() {
     return fa_fwd_w4p_kernel<(C != 0), DT == 1, 2, HDIM>;
   else if constexpr (KIND == 8)
     return fa_fwd_w4p_kernel<(C != 0), DT == 1, 0, HDIM>;
+  else if constexpr (KIND == 9)
+    return fa_fwd_w4p_kernel<(C != 0), DT == 1, 3, HDIM>;
 
   else if constexpr (KIND == 3)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
@@ -405,10 +408,11 @@ constexpr kernel_fn pick_kernel() {
   {{ID, 128 * (G), 64, 4, C, 0, w4p_lds_bytes<G, HDIM>(), NAME, DT, HDIM}, 0, 5 + (G),    \
    pick_kernel<4, 64, C, 5 + (G), 0, DT, HDIM>()}
 #define FA_CFG_W4P(ID, G, C, DT, NAME) FA_CFG_W4PD(ID, G, C, DT, 128, NAME)
-// W4P singles: 4 waves x 16 query rows of one 64-row block
-#define FA_CFG_W4PS(ID, C, DT, HDIM, NAME)                                             \
-  {{ID, 64, 64, 4, C, 0, w4p_lds_bytes<0, HDIM>(), NAME, DT, HDIM}, 0, 8,                 \
-   pick_kernel<4, 64, C, 8, 0, DT, HDIM>()}
+// W4P singles: 4 waves x 16 query rows of one 64-row block (KIND 8), or of
+// one or two (KIND 9: the heaviest blocks alone, the rest paired)
+#define FA_CFG_W4PS(ID, C, DT, HDIM, NAME, KIND)                                       \
+  {{ID, 64, 64, 4, C, 0, w4p_lds_bytes<(KIND) == 9 ? 3 : 0, HDIM>(), NAME, DT, HDIM}, 0, KIND, \
+   pick_kernel<4, 64, C, KIND, 0, DT, HDIM>()}
 
 // Only tiers the dispatcher picks, explicit entry points (split-KV) and the
 // baselines a test compares against (the per-item ping-pong 2/3: the
@@ -491,14 +495,20 @@ static const Config kConfigs[] = {
     FA_CFG_W4PD(63, 2, 1, 1, 64, "bf16_d64_bm256_bn64_w4x64_m16_asm_quad_causal"),
     // one 64-row block per workgroup on the pair program (launches of at most
     // one block per CU)
-    FA_CFG_W4PS(64, 0, 0, 128, "bm64_bn64_w4x16_m16_asm_single_noncausal"),
-    FA_CFG_W4PS(65, 1, 0, 128, "bm64_bn64_w4x16_m16_asm_single_causal"),
-    FA_CFG_W4PS(66, 0, 1, 128, "bf16_bm64_bn64_w4x16_m16_asm_single_noncausal"),
-    FA_CFG_W4PS(67, 1, 1, 128, "bf16_bm64_bn64_w4x16_m16_asm_single_causal"),
-    FA_CFG_W4PS(68, 0, 0, 64, "d64_bm64_bn64_w4x16_m16_asm_single_noncausal"),
-    FA_CFG_W4PS(69, 1, 0, 64, "d64_bm64_bn64_w4x16_m16_asm_single_causal"),
-    FA_CFG_W4PS(70, 0, 1, 64, "bf16_d64_bm64_bn64_w4x16_m16_asm_single_noncausal"),
-    FA_CFG_W4PS(71, 1, 1, 64, "bf16_d64_bm64_bn64_w4x16_m16_asm_single_causal"),
+    FA_CFG_W4PS(64, 0, 0, 128, "bm64_bn64_w4x16_m16_asm_single_noncausal", 8),
+    FA_CFG_W4PS(65, 1, 0, 128, "bm64_bn64_w4x16_m16_asm_single_causal", 8),
+    FA_CFG_W4PS(66, 0, 1, 128, "bf16_bm64_bn64_w4x16_m16_asm_single_noncausal", 8),
+    FA_CFG_W4PS(67, 1, 1, 128, "bf16_bm64_bn64_w4x16_m16_asm_single_causal", 8),
+    FA_CFG_W4PS(68, 0, 0, 64, "d64_bm64_bn64_w4x16_m16_asm_single_noncausal", 8),
+    FA_CFG_W4PS(69, 1, 0, 64, "d64_bm64_bn64_w4x16_m16_asm_single_causal", 8),
+    FA_CFG_W4PS(70, 0, 1, 64, "bf16_d64_bm64_bn64_w4x16_m16_asm_single_noncausal", 8),
+    FA_CFG_W4PS(71, 1, 1, 64, "bf16_d64_bm64_bn64_w4x16_m16_asm_single_causal", 8),
+    // causal launches between one and two 64-row blocks per CU: the heaviest
+    // blocks alone, the rest in pairs, one workgroup per CU
+    FA_CFG_W4PS(72, 1, 0, 128, "bm64_bn64_w4x16_m16_asm_mixed_causal", 9),
+    FA_CFG_W4PS(73, 1, 1, 128, "bf16_bm64_bn64_w4x16_m16_asm_mixed_causal", 9),
+    FA_CFG_W4PS(74, 1, 0, 64, "d64_bm64_bn64_w4x16_m16_asm_mixed_causal", 9),
+    FA_CFG_W4PS(75, 1, 1, 64, "bf16_d64_bm64_bn64_w4x16_m16_asm_mixed_causal", 9),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -592,6 +602,12 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
   // few heads per XCD: plain heaviest-first balances better; many: keep the
   // query blocks of a head together for L2 reuse (profiles/r01_band_ab.txt)
   p.band = bh <= 64 ? FA_BAND_FEW_HEADS : 16;
+  if (cfg.kind == 9) {
+    // workgroups per head: the CUs' share, between ceil(nqb64 / 2) (pairs)
+    // and nqb64 (singles)
+    const int nq = (seq_len + 63) / 64;
+    p.nqb = std::max((nq + 1) / 2, std::min(nq, num_cus() / std::max(bh, 1)));
+  }
   long long blocks = (long long)p.nqb * bh * num_splits;
   if (blocks > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
   if (cfg.kind == 2 || cfg.kind == 5) blocks = persistent_blocks(cfg, bh, p.nqb);
@@ -741,7 +757,19 @@ static int select_tier(int batch, int heads, int seq_len, int causal, bool pair)
   //    (B=4 H=32 S=1024 802 vs 701)
   if (pair) {
     const long long nq64 = (seq_len + 63) / 64, pairs = bh * ((nq64 + 1) / 2), cus = num_cus();
-    if (causal && nq64 <= 64 && pairs <= cus) return cfg_for(128, 4, 64, c, 0, 6);
+    // causal, between one and two blocks per CU: the heaviest blocks alone,
+    // the rest paired, one workgroup per CU (a pair's two-block iterations
+    // cost less than two singles', so the heaviest block sets the launch);
+    // bit-identical to the pairs, same process (profiles/r06_ab_w4p_mixed.jsonl):
+    // H=32 S=768 417 vs pairs 375, S=640 335 vs 303, S=896 506 vs 474, H=24
+    // S=1024 483 vs 445, H=20 S=1024 415 vs 384, B=3 H=8 S=1024 486 vs 447,
+    // H=10 S=2048 444 vs 432, H=12 S=2048 553 vs 556, H=6 S=4096 607 vs 599;
+    // d64 S=768 287 vs 259.  Where no block can go alone (B=1 H=32 S=1024:
+    // 8 CUs for 16 blocks per head) it is the pair grouping itself.
+    if (causal && nq64 <= 64 && pairs <= cus) {
+      const bool mixed = cus / bh > (nq64 + 1) / 2;
+      return mixed ? cfg_for(64, 4, 64, c, 0, 9) : cfg_for(128, 4, 64, c, 0, 6);
+    }
     if (causal && nq64 <= 64 && pairs <= 2 * cus) return cfg_for(256, 4, 64, c, 0, 7);
     if (!causal && 4 * pairs >= 3 * cus) return cfg_for(128, 4, 64, c, 0, 6);
   }

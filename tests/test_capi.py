@@ -86,7 +86,7 @@ def test_config_table():
         # K and V image buffers of 256-B row slots: double-buffered, or three
         # rotating buffers each for the LDS-DMA configs
         nbuf = 3 if "_dma_" in c.name else 2
-        if any(t in c.name for t in ("_asm_persistent_", "_asm_pair_", "_asm_single_")) and c.head_dim == 128:
+        if any(t in c.name for t in ("_asm_persistent_", "_asm_pair_", "_asm_single_", "_asm_mixed_")) and c.head_dim == 128:
             nbuf = 4  # the W4 / W4P pair programs' two key tiles per barrier (gen_w4*_item.py)
         need = 2 * nbuf * c.block_n * 256
         if "_pingpong_persistent_" in c.name and "_dma_" not in c.name and not c.causal:
@@ -132,6 +132,9 @@ def test_select_config(causal):
         assert want in cfgs[fa.select_config(b, h, s, causal)].name, (b, h, s, causal)
     for b, h, s in ((1, 16, 2048), (1, 8, 4096), (2, 8, 2048)):  # <= 1 round of pairs
         assert "_asm_pair_" in cfgs[fa.select_config(b, h, s, causal)].name, (b, h, s, causal)
+    if causal:  # one to two blocks per CU: the heaviest blocks alone, the rest paired
+        for b, h, s in ((1, 32, 768), (1, 24, 1024), (3, 8, 1024), (1, 12, 2048)):
+            assert "_asm_mixed_" in cfgs[fa.select_config(b, h, s, True)].name, (b, h, s)
     if causal:  # 1-2 rounds of pairs: two pairs per workgroup
         for b, h, s in ((1, 32, 2048), (2, 32, 1024), (1, 16, 4096)):
             assert "_asm_quad_" in cfgs[fa.select_config(b, h, s, True)].name, (b, h, s)

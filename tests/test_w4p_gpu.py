@@ -265,6 +265,42 @@ def test_single_dispatched(b, h, s):
         assert (out.float() - _torch_ref(q, k, v, causal)).abs().max().item() <= TOL
 
 
+MIXED = "bm64_bn64_w4x16_m16_asm_mixed_causal"
+
+
+@pytest.mark.parametrize("d", [128, 64])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["fp16", "bf16"])
+def test_mixed_matches_pair_bitwise(dtype, d):
+    """causal launches of one to two blocks per CU: the heaviest blocks alone,
+    the rest paired (the pair program either way): bit-identical to the pairs"""
+    fa = _fa()
+    pre = ("bf16_" if dtype == torch.bfloat16 else "") + ("d64_" if d == 64 else "")
+    mixed = next(c.id for c in fa.configs() if c.name == pre + MIXED)
+    for b, h, s in ((1, 32, 768), (1, 24, 1000), (2, 3, 1000), (1, 5, 513), (1, 1, 4095), (1, 32, 1024)):
+        q, k, v = (_rand((b, h, s, d), 900 + i, 4.0 if i < 2 else 1.0, dtype) for i in range(3))
+        a = fa.flash_attention_fwd(q, k, v, causal=True, config=mixed)
+        p = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(pre + PAIR)[True])
+        assert torch.equal(a, p), (b, h, s)
+
+
+@pytest.mark.parametrize("b,h,s", [(1, 32, 768), (1, 24, 1024), (3, 8, 1024), (1, 12, 2048), (1, 32, 640),
+                                   (1, 9, 2000)])
+def test_mixed_dispatched(b, h, s):
+    """the dispatched mixed grouping against fp32 torch on every head and the
+    oracle on sampled heads"""
+    fa = _fa()
+    assert "_asm_mixed_" in fa.configs()[fa.select_config(b, h, s, True)].name, (b, h, s)
+    q, k, v = (_rand((b, h, s, 128), 910 + i) for i in range(3))
+    out = fa.flash_attention_fwd(q, k, v, causal=True)
+    torch.cuda.synchronize()
+    assert (out.float() - _torch_ref(q, k, v, True)).abs().max().item() <= TOL
+    for flat in sorted({0, b * h - 1}):
+        bi, hi = divmod(flat, h)
+        sl = (slice(bi, bi + 1), slice(hi, hi + 1))
+        ro = oracle.attention(*(_bits(x[sl]) for x in (q, k, v)), True)
+        assert oracle.max_abs_diff(_bits(out[sl]), ro) <= TOL
+
+
 def test_pair_d64_row0_ones_deterministic():
     fa = _fa()
     q, k, v = (_rand((1, 8, 2048, 64), 840 + i) for i in range(3))
