@@ -168,14 +168,17 @@ int fa_fwd_bf16_ws(const void* q, const void* k, const void* v, void* o,
  * query fails).  The tier is the same for fp16 and bf16; fa_fwd_f16 /
  * fa_fwd_bf16 at head_dim 64 run the head_dim-64 twin of this tier, except
  * that non-causal head_dim-64 launches skip the paired tier (its d64 twin
- * trails the tier below there) and run the tier below it.
+ * trails the tier below there) and take the one-block-per-workgroup tier
+ * only up to 16 blocks per head (S <= 1024), running the tier below it
+ * otherwise.
  *
  * Config ids are positions in this build's table (fa_num_configs /
  * fa_config_info): they are not stable across releases (round 3 renumbered
  * 0-49 to 0-43 when the table was trimmed to the dispatched tiers; round 4
  * appended the head_dim-64 W4 configs 44-47; round 5 the paired
  * short-sequence configs 48-51, their four-block twins 52-55 and the
- * head_dim-64 twins of both, 56-63).  Select a tier by its
+ * head_dim-64 twins of both, 56-63; round 6 the one-block-per-workgroup
+ * configs 64-71 and the causal singles-and-pairs mix 72-75).  Select a tier by its
  * fa_config_info().name, not by a remembered id. */
 int fa_select_config(int batch, int heads, int seq_len, int causal);
 
