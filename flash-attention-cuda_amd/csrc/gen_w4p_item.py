@@ -165,7 +165,7 @@ VBUF = [32768, 49152]
 # wait and one barrier, the second tile's key-block-0 fragments read in the
 # first tile's PV tail.  W4_XP=nodblp: the one-tile loop.
 def pdbl():
-    return nb() == 2 and NT == 4 and "nodblp" not in w4.XP and "p1nolds" not in w4.XP
+    return (nb() == 2 or "dblq" in w4.XP) and NT == 4 and "nodblp" not in w4.XP and "p1nolds" not in w4.XP
 
 
 def nbuf():
@@ -1119,11 +1119,12 @@ HEADER = """// GENERATED by gen_w4p_item.py -- do not edit.
 def header():
     # the head_dim-128 pair programs' LDS layout (fa_w4p_kernel.hpp): 1 = four
     # K / V images per tensor (two key tiles per barrier), 128 KiB
-    CURNB["nb"] = 2
     set_hd(128)
+    CURNB["nb"] = 2
     on = pdbl()
     CURNB["nb"] = 4
-    return HEADER + f"#define FA_W4P_DBL {1 if on else 0}\n"
+    on4 = pdbl()
+    return HEADER + f"#define FA_W4P_DBL {1 if on else 0}\n#define FA_W4P_DBL4 {1 if on4 else 0}\n"
 
 
 def cxx(causal, bf16, lines):
