@@ -13,6 +13,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <map>
 #include <mutex>
 
 #include "fa_fwd_kernel.hpp"
@@ -346,7 +347,9 @@ struct Config {
               // 6 = paired 64-row query blocks, one wave per SIMD (W4P, asm item program),
               // 7 = two pairs per workgroup (the same program), 8 = one 64-row
               // block per workgroup (the same program), 9 = causal singles
-              // and pairs mixed to fill the CUs (the same program)
+              // and pairs mixed to fill the CUs (the same program), 10 =
+              // causal groups of one to four blocks planned on the host
+              // (w4p_plan: the two- or the four-block program per group)
   kernel_fn fn;
 };
 
@@ -362,6 +365,8 @@ constexpr kernel_fn pick_kernel() {
     return fa_fwd_w4p_kernel<(C != 0), DT == 1, 0, HDIM>;
   else if constexpr (KIND == 9)
     return fa_fwd_w4p_kernel<(C != 0), DT == 1, 3, HDIM>;
+  else if constexpr (KIND == 10)
+    return fa_fwd_w4p_kernel<(C != 0), DT == 1, 4, HDIM>;
 
   else if constexpr (KIND == 3)
     return fa_fwd_f16_kvpair_kernel<BN_, (C != 0), DT == 1, HDIM>;
@@ -411,8 +416,8 @@ constexpr kernel_fn pick_kernel() {
 // W4P singles: 4 waves x 16 query rows of one 64-row block (KIND 8), or of
 // one or two (KIND 9: the heaviest blocks alone, the rest paired)
 #define FA_CFG_W4PS(ID, C, DT, HDIM, NAME, KIND)                                       \
-  {{ID, 64, 64, 4, C, 0, w4p_lds_bytes<(KIND) == 9 ? 3 : 0, HDIM>(), NAME, DT, HDIM}, 0, KIND, \
-   pick_kernel<4, 64, C, KIND, 0, DT, HDIM>()}
+  {{ID, 64, 64, 4, C, 0, w4p_lds_bytes<(KIND) == 10 ? 4 : (KIND) == 9 ? 3 : 0, HDIM>(), NAME, DT, \
+    HDIM}, 0, KIND, pick_kernel<4, 64, C, KIND, 0, DT, HDIM>()}
 
 // Only tiers the dispatcher picks, explicit entry points (split-KV) and the
 // baselines a test compares against (the per-item ping-pong 2/3: the
@@ -509,6 +514,12 @@ static const Config kConfigs[] = {
     FA_CFG_W4PS(73, 1, 1, 128, "bf16_bm64_bn64_w4x16_m16_asm_mixed_causal", 9),
     FA_CFG_W4PS(74, 1, 0, 64, "d64_bm64_bn64_w4x16_m16_asm_mixed_causal", 9),
     FA_CFG_W4PS(75, 1, 1, 64, "bf16_d64_bm64_bn64_w4x16_m16_asm_mixed_causal", 9),
+    // causal launches of two to four blocks per CU short of whole quads:
+    // groups of one to four blocks planned on the host, one workgroup per CU
+    FA_CFG_W4PS(76, 1, 0, 128, "bm64_bn64_w4x16_m16_asm_planned_causal", 10),
+    FA_CFG_W4PS(77, 1, 1, 128, "bf16_bm64_bn64_w4x16_m16_asm_planned_causal", 10),
+    FA_CFG_W4PS(78, 1, 0, 64, "d64_bm64_bn64_w4x16_m16_asm_planned_causal", 10),
+    FA_CFG_W4PS(79, 1, 1, 64, "bf16_d64_bm64_bn64_w4x16_m16_asm_planned_causal", 10),
 };
 static constexpr int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
@@ -542,6 +553,118 @@ static int num_cus() {
     cache[dev] = n;
   }
   return cache[dev];
+}
+
+// ---------------------------------------------------------------------------
+// W4P planned groups (kind 10): a head's nq causal 64-row blocks (block b has
+// b + 1 key tiles) in W workgroups of one to four blocks, minimising the
+// heaviest workgroup under a cycle model from the stamps
+// (profiles/r06_final_w4p_stamps.jsonl, r05_w4q2_stamps.jsonl): an
+// iteration with L live blocks costs 1092 / 1617 cycles in the two-block
+// program and 1550 / 1620 / 2875 / 2789 in the four-block one, plus a
+// per-group prologue + epilogue of 7.0k / 8.8k / 13.5k / 16.0k cycles.
+// Greedy placement (the W heaviest blocks one per group, the rest each to
+// the group it costs least), then a deterministic local search of moves and
+// swaps that never raise the pair of groups' larger cost.  Cached per
+// (nq, W); the quads' cost under the same model decides whether to use it.
+// ---------------------------------------------------------------------------
+struct W4PPlan {
+  long long cost = 0, quads_cost = 0;
+  unsigned char g[256];
+};
+
+static long long w4p_group_cost(const int* blocks, int n) {
+  static const int c2[3] = {0, 1092, 1617}, c4[5] = {0, 1550, 1620, 2875, 2789};
+  static const int fix[5] = {0, 7000, 8800, 13500, 16000};
+  if (n == 0) return 0;
+  int t[4];
+  for (int i = 0; i < n; ++i) t[i] = blocks[i] + 1;
+  std::sort(t, t + n, [](int a, int b) { return a > b; });
+  long long tot = fix[n];
+  for (int i = 0; i < n; ++i) {
+    const int next = i + 1 < n ? t[i + 1] : 0;
+    tot += (long long)(t[i] - next) * (n <= 2 ? c2[i + 1] : c4[i + 1]);
+  }
+  return tot;
+}
+
+static W4PPlan w4p_plan(int nq, int W) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, W4PPlan> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find({nq, W});
+  if (it != cache.end()) return it->second;
+  W4PPlan pl;
+  std::fill(pl.g, pl.g + 256, (unsigned char)0xff);
+  if (nq < 1 || nq > 64 || W < (nq + 3) / 4 || W > nq || W > 64) {
+    pl.cost = pl.quads_cost = 0;
+    return cache[{nq, W}] = pl;
+  }
+  int grp[64][4], cnt[64] = {};
+  long long cost[64] = {};
+  for (int i = 0; i < W; ++i) {
+    grp[i][0] = nq - 1 - i;
+    cnt[i] = 1;
+    cost[i] = w4p_group_cost(grp[i], 1);
+  }
+  for (int b = nq - 1 - W; b >= 0; --b) {
+    int best = -1;
+    long long bc = 0;
+    for (int i = 0; i < W; ++i) {
+      if (cnt[i] == 4) continue;
+      grp[i][cnt[i]] = b;
+      const long long c = w4p_group_cost(grp[i], cnt[i] + 1);
+      if (best < 0 || c < bc) best = i, bc = c;
+    }
+    grp[best][cnt[best]++] = b;
+    cost[best] = bc;
+  }
+  unsigned seed = 12345;
+  auto rnd = [&seed](int n) {
+    seed = seed * 1103515245u + 12345u;
+    return (int)(((seed & 0x7fffffffu) >> 8) % (unsigned)n);
+  };
+  for (int it2 = 0; it2 < 20000; ++it2) {
+    const int a = rnd(W), b = rnd(W);
+    if (a == b) continue;
+    int na[4], nb[4], ca = cnt[a], cbn = cnt[b];
+    std::copy(grp[a], grp[a] + 4, na);
+    std::copy(grp[b], grp[b] + 4, nb);
+    if (rnd(2) == 0 && cnt[b] < 4 && cnt[a] > 1) {  // move one block a -> b
+      const int x = rnd(cnt[a]);
+      nb[cbn++] = na[x];
+      na[x] = na[--ca];
+    } else {  // swap one block of a with one of b
+      const int x = rnd(cnt[a]), y = rnd(cnt[b]);
+      std::swap(na[x], nb[y]);
+    }
+    const long long xa = w4p_group_cost(na, ca), xb = w4p_group_cost(nb, cbn);
+    if (std::max(xa, xb) <= std::max(cost[a], cost[b])) {
+      std::copy(na, na + 4, grp[a]);
+      std::copy(nb, nb + 4, grp[b]);
+      cnt[a] = ca, cnt[b] = cbn, cost[a] = xa, cost[b] = xb;
+    }
+  }
+  // ranks heaviest first (the first-dispatched workgroups)
+  int order[64];
+  for (int i = 0; i < W; ++i) order[i] = i;
+  std::sort(order, order + W, [&](int x, int y) { return cost[x] > cost[y] || (cost[x] == cost[y] && x < y); });
+  for (int r = 0; r < W; ++r) {
+    const int i = order[r];
+    for (int k = 0; k < cnt[i]; ++k) pl.g[4 * r + k] = (unsigned char)grp[i][k];
+    pl.cost = std::max(pl.cost, cost[i]);
+  }
+  // the quads (G = 2): item i = pairs 2i, 2i+1, pair r = (nq-1-r, r)
+  const int np = (nq + 1) / 2;
+  for (int i = 0; 2 * i < np; ++i) {
+    int q[4], n = 0;
+    for (int r = 2 * i; r < 2 * i + 2 && r < np; ++r) {
+      q[n++] = nq - 1 - r;
+      if (r < nq - 1 - r) q[n++] = r;
+    }
+    pl.quads_cost = std::max(pl.quads_cost, w4p_group_cost(q, n));
+  }
+  return cache[{nq, W}] = pl;
 }
 
 static int check_args(const void* q, const void* k, const void* v, const void* o, int batch,
@@ -607,6 +730,14 @@ static int launch(int id, const void* q, const void* k, const void* v, void* o, 
     // and nqb64 (singles)
     const int nq = (seq_len + 63) / 64;
     p.nqb = std::max((nq + 1) / 2, std::min(nq, num_cus() / std::max(bh, 1)));
+  }
+  if (cfg.kind == 10) {
+    // workgroups per head: the CUs' share, between ceil(nqb64 / 4) and nqb64
+    const int nq = (seq_len + 63) / 64;
+    if (nq > 64) return FA_ERR_BAD_CONFIG;
+    p.nqb = std::max((nq + 3) / 4, std::min(nq, num_cus() / std::max(bh, 1)));
+    const W4PPlan pl = w4p_plan(nq, p.nqb);
+    std::copy(pl.g, pl.g + 256, p.plan);
   }
   long long blocks = (long long)p.nqb * bh * num_splits;
   if (blocks > 0x7fffffffLL) return FA_ERR_BAD_SHAPE;
@@ -721,13 +852,13 @@ static int select_tier(int batch, int heads, int seq_len, int causal, bool pair)
   // (pair = false) up to 16 blocks per head: S=512 308 vs KV-quad 276, H=16
   // S=1024 417 vs 406; H=8 S=2048 507 vs 525, H=4 S=4096 485 vs 607
   if (wg64 <= num_cus() && (seq_len + 63) / 64 <= (pair ? 64 : 16)) return cfg_for(64, 4, 64, c, 0, 8);
-  if (seq_len <= 128) return cfg_for(128, 4, 64, c, 0, 0);
   // causal with about one 256-row item per CU: the snake cannot balance item
   // costs 1..nqb256, so the KV-pair's halved heaviest key loop wins from
   // nqb256 = 4 on (B=2 S=1024: 503 vs 461; B=4 S=512: 264 vs 364)
   // non-causal: from 160 items (B=1 H=24 S=2048: 829 vs KV-pair 668; H=6
   // S=8192: 1039 vs 854; at 128 items the KV-pair still wins, 732 vs 532)
-  const bool persist = causal ? (wg256 >= 384 || (wg256 >= 256 && nqb256 <= 2)) : wg256 >= 160;
+  const bool persist =
+      seq_len > 128 && (causal ? (wg256 >= 384 || (wg256 >= 256 && nqb256 <= 2)) : wg256 >= 160);
   if (persist) {
     // the one-wave-per-SIMD asm kernel (W4, same items and order), except a
     // non-causal launch whose last round is short: the ping-pong runs that
@@ -739,7 +870,6 @@ static int select_tier(int batch, int heads, int seq_len, int causal, bool pair)
     if (!causal && tail > 0 && 2 * tail <= cus) return cfg_for(256, 8, 64, c, 1, 2);
     return cfg_for(256, 4, 64, c, 0, 5);
   }
-  if (seq_len <= 256) return cfg_for(128, 4, 64, c, 0, 0);
   // paired 64-row query blocks (W4P, fa_w4p_kernel.hpp), same-process A/Bs
   // against the KV-pair / KV-quad / split tiers (profiles/r05_w4p_*ab*.jsonl):
   //  * causal, S <= 4096, one round of pairs on the CUs (every pair costs
@@ -755,6 +885,12 @@ static int select_tier(int batch, int heads, int seq_len, int causal, bool pair)
   //    two after): B=1 H=32 S=2048 816 vs pairs 663, B=2 H=32 S=1024 662 vs
   //    532, H=16 S=4096 942 vs KV-pair 862; past that the persistent tier
   //    (B=4 H=32 S=1024 802 vs 701)
+  //  * S <= 256 (round 6): one round of pairs (or the mixed grouping) beats
+  //    the 4-wave loop there too (H=96 S=256 causal 193 vs 147, H=65 S=256
+  //    mixed 152 vs 105, B=2 H=64 S=256 257 vs 195, H=200 S=128 120 vs 105;
+  //    non-causal H=96 S=256 357 vs 324, H=200 S=128 233 vs 228;
+  //    profiles/r06_ab_w4p_short.jsonl); quads stay above S=256 (unmeasured
+  //    below)
   if (pair) {
     const long long nq64 = (seq_len + 63) / 64, pairs = bh * ((nq64 + 1) / 2), cus = num_cus();
     // causal, between one and two blocks per CU: the heaviest blocks alone,
@@ -770,9 +906,22 @@ static int select_tier(int batch, int heads, int seq_len, int causal, bool pair)
       const bool mixed = cus / bh > (nq64 + 1) / 2;
       return mixed ? cfg_for(64, 4, 64, c, 0, 9) : cfg_for(128, 4, 64, c, 0, 6);
     }
-    if (causal && nq64 <= 64 && pairs <= 2 * cus) return cfg_for(256, 4, 64, c, 0, 7);
-    if (!causal && 4 * pairs >= 3 * cus) return cfg_for(128, 4, 64, c, 0, 6);
+    if (causal && nq64 <= 64 && pairs <= 2 * cus && seq_len > 256) {
+      // groups planned on the host where the quads leave CUs idle and the
+      // plan's modelled heaviest workgroup is >= 5 % lighter than theirs;
+      // bit-identical to the pairs, same process (profiles/r06_ab_w4p_planned.jsonl):
+      // H=32 S=1280 655 vs quads 533, S=1536 701 vs 675, S=1792 802 vs 764,
+      // H=25 S=2048 731 vs 704, H=16 S=2560 807 vs 641, S=3072 896 vs 792,
+      // d64 S=1536 507 vs 462; where whole quads fill the CUs the model keeps
+      // them (S=2048 862 vs planned 858, B=2 S=1024 684 vs 673)
+      const int W = (int)std::min<long long>(nq64, cus / bh);
+      const W4PPlan pl = w4p_plan((int)nq64, W);
+      if (pl.cost > 0 && 100 * pl.cost <= 95 * pl.quads_cost) return cfg_for(64, 4, 64, c, 0, 10);
+      return cfg_for(256, 4, 64, c, 0, 7);
+    }
+    if (!causal && 4 * pairs >= 3 * cus && (seq_len > 256 || pairs <= cus)) return cfg_for(128, 4, 64, c, 0, 6);
   }
+  if (seq_len <= 256) return cfg_for(128, 4, 64, c, 0, 0);
   // causal, two rounds of 64-row blocks over long heads (>= 32 blocks per
   // head): the KV-quad's four-way key split halves the heaviest block's key
   // loop against the KV-pair (B=1 H=4 S=8192 765 vs 599, H=2 S=16384 808 vs

@@ -89,6 +89,9 @@ struct FwdParams {
   char* ws_o;
   int piece_tiles;
   int pmax;
+  // W4P planned grouping (fa_w4p_kernel.hpp G = 4): workgroup rank r of a
+  // head runs the 64-row blocks plan[4 r .. 4 r + 3] (0xff = none)
+  unsigned char plan[256];
 };
 
 // ---------------------------------------------------------------------------

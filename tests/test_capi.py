@@ -86,7 +86,7 @@ def test_config_table():
         # K and V image buffers of 256-B row slots: double-buffered, or three
         # rotating buffers each for the LDS-DMA configs
         nbuf = 3 if "_dma_" in c.name else 2
-        if any(t in c.name for t in ("_asm_persistent_", "_asm_pair_", "_asm_single_", "_asm_mixed_")) and c.head_dim == 128:
+        if any(t in c.name for t in ("_asm_persistent_", "_asm_pair_", "_asm_single_", "_asm_mixed_", "_asm_planned_")) and c.head_dim == 128:
             nbuf = 4  # the W4 / W4P pair programs' two key tiles per barrier (gen_w4*_item.py)
         need = 2 * nbuf * c.block_n * 256
         if "_pingpong_persistent_" in c.name and "_dma_" not in c.name and not c.causal:
@@ -120,7 +120,10 @@ def test_select_config(causal):
     for b, h, s in ((1, 8, 2048), (1, 32, 512), (1, 32, 256), (1, 4, 4096), (1, 64, 256), (1, 32, 128),
                     (4, 32, 128), (1, 1, 1)):
         assert "_asm_single_" in cfgs[fa.select_config(b, h, s, causal)].name, (b, h, s, causal)
-    assert "_w4_" in cfgs[fa.select_config(8, 32, 128, causal)].name
+    assert "_w4_" in cfgs[fa.select_config(16, 32, 128, causal)].name
+    # S <= 256 past one block per CU: one round of pairs (causal: or mixed)
+    assert "_asm_pair_" in cfgs[fa.select_config(1, 96, 256, causal)].name
+    assert "_asm_pair_" in cfgs[fa.select_config(1, 200, 128, causal)].name
     assert "_asm_single_" not in cfgs[fa.select_config(1, 4, 8192, causal)].name  # 128 blocks per head
     assert "_asm_pair_" in cfgs[fa.select_config(1, 16, 2048, causal)].name  # 512 blocks
     # between the KV-quad's and the paired tier's non-causal shapes: the KV-pair
@@ -135,6 +138,9 @@ def test_select_config(causal):
     if causal:  # one to two blocks per CU: the heaviest blocks alone, the rest paired
         for b, h, s in ((1, 32, 768), (1, 24, 1024), (3, 8, 1024), (1, 12, 2048)):
             assert "_asm_mixed_" in cfgs[fa.select_config(b, h, s, True)].name, (b, h, s)
+    if causal:  # 2-4 blocks per CU short of whole quads: groups planned on the host
+        for b, h, s in ((1, 32, 1280), (1, 32, 1536), (1, 16, 2560), (1, 25, 2048)):
+            assert "_asm_planned_" in cfgs[fa.select_config(b, h, s, True)].name, (b, h, s)
     if causal:  # 1-2 rounds of pairs: two pairs per workgroup
         for b, h, s in ((1, 32, 2048), (2, 32, 1024), (1, 16, 4096)):
             assert "_asm_quad_" in cfgs[fa.select_config(b, h, s, True)].name, (b, h, s)

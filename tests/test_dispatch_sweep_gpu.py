@@ -60,6 +60,10 @@ BOUNDARY = [
     (1, 32, 512, 128, True, False), (3, 5, 77, 128, True, False), (1, 1, 1, 128, False, False),
     (1, 32, 1024, 64, True, False), (1, 8, 4096, 64, True, False), (2, 16, 2048, 64, False, False),
     (1, 32, 1024, 128, True, True), (1, 4, 8192, 128, True, True), (1, 32, 2048, 64, True, True),
+    # round 6: the singles / mixed edges (<= 1 block per CU; 1-2 per CU)
+    (1, 32, 513, 128, True, False), (1, 32, 576, 128, True, False), (1, 17, 1024, 128, True, False),
+    (1, 65, 256, 128, True, False), (1, 16, 1024, 64, False, False), (1, 16, 1088, 64, False, False),
+    (1, 32, 768, 64, True, True), (1, 4, 4096, 128, False, True),
 ]
 
 

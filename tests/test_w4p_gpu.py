@@ -301,6 +301,42 @@ def test_mixed_dispatched(b, h, s):
         assert oracle.max_abs_diff(_bits(out[sl]), ro) <= TOL
 
 
+PLANNED = "bm64_bn64_w4x16_m16_asm_planned_causal"
+
+
+@pytest.mark.parametrize("d", [128, 64])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["fp16", "bf16"])
+def test_planned_matches_pair_bitwise(dtype, d):
+    """causal launches of two to four blocks per CU short of whole quads:
+    groups of one to four blocks planned on the host, each on the two- or the
+    four-block program -- every block's arithmetic is the pairs', bit for bit"""
+    fa = _fa()
+    pre = ("bf16_" if dtype == torch.bfloat16 else "") + ("d64_" if d == 64 else "")
+    planned = next(c.id for c in fa.configs() if c.name == pre + PLANNED)
+    for b, h, s in ((1, 32, 1536), (1, 25, 2048), (2, 3, 1000), (1, 16, 3000), (1, 32, 1280), (1, 1, 4096)):
+        q, k, v = (_rand((b, h, s, d), 920 + i, 4.0 if i < 2 else 1.0, dtype) for i in range(3))
+        a = fa.flash_attention_fwd(q, k, v, causal=True, config=planned)
+        p = fa.flash_attention_fwd(q, k, v, causal=True, config=_ids(pre + PAIR)[True])
+        assert torch.equal(a, p), (b, h, s)
+
+
+@pytest.mark.parametrize("b,h,s", [(1, 32, 1280), (1, 32, 1536), (1, 16, 2560), (1, 25, 2048), (1, 13, 3500)])
+def test_planned_dispatched(b, h, s):
+    """the dispatched planned grouping against fp32 torch on every head and
+    the oracle on sampled heads"""
+    fa = _fa()
+    assert "_asm_planned_" in fa.configs()[fa.select_config(b, h, s, True)].name, (b, h, s)
+    q, k, v = (_rand((b, h, s, 128), 930 + i) for i in range(3))
+    out = fa.flash_attention_fwd(q, k, v, causal=True)
+    torch.cuda.synchronize()
+    assert (out.float() - _torch_ref(q, k, v, True)).abs().max().item() <= TOL
+    for flat in sorted({0, b * h - 1}):
+        bi, hi = divmod(flat, h)
+        sl = (slice(bi, bi + 1), slice(hi, hi + 1))
+        ro = oracle.attention(*(_bits(x[sl]) for x in (q, k, v)), True)
+        assert oracle.max_abs_diff(_bits(out[sl]), ro) <= TOL
+
+
 def test_pair_d64_row0_ones_deterministic():
     fa = _fa()
     q, k, v = (_rand((1, 8, 2048, 64), 840 + i) for i in range(3))
