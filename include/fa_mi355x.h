@@ -178,7 +178,8 @@ int fa_fwd_bf16_ws(const void* q, const void* k, const void* v, void* o,
  * appended the head_dim-64 W4 configs 44-47; round 5 the paired
  * short-sequence configs 48-51, their four-block twins 52-55 and the
  * head_dim-64 twins of both, 56-63; round 6 the one-block-per-workgroup
- * configs 64-71 and the causal singles-and-pairs mix 72-75).  Select a tier by its
+ * configs 64-71, the causal singles-and-pairs mix 72-75 and the causal
+ * groups planned on the host 76-79).  Select a tier by its
  * fa_config_info().name, not by a remembered id. */
 int fa_select_config(int batch, int heads, int seq_len, int causal);
 
