@@ -919,7 +919,11 @@ static int select_tier(int batch, int heads, int seq_len, int causal, bool pair)
       if (pl.cost > 0 && 100 * pl.cost <= 95 * pl.quads_cost) return cfg_for(64, 4, 64, c, 0, 10);
       return cfg_for(256, 4, 64, c, 0, 7);
     }
-    if (!causal && 4 * pairs >= 3 * cus && (seq_len > 256 || pairs <= cus)) return cfg_for(128, 4, 64, c, 0, 6);
+    // non-causal below 3/4 of a round too, past the singles (heads of <= 64
+    // blocks; r06_ab_w4p_short.jsonl: H=20 S=1024 570 vs KV-pair 520, H=18
+    // 520 vs 478, H=10 S=2048 704 vs 629)
+    if (!causal && (4 * pairs >= 3 * cus ? (seq_len > 256 || pairs <= cus) : nq64 <= 64))
+      return cfg_for(128, 4, 64, c, 0, 6);
   }
   if (seq_len <= 256) return cfg_for(128, 4, 64, c, 0, 0);
   // causal, two rounds of 64-row blocks over long heads (>= 32 blocks per

@@ -126,8 +126,10 @@ def test_select_config(causal):
     assert "_asm_pair_" in cfgs[fa.select_config(1, 200, 128, causal)].name
     assert "_asm_single_" not in cfgs[fa.select_config(1, 4, 8192, causal)].name  # 128 blocks per head
     assert "_asm_pair_" in cfgs[fa.select_config(1, 16, 2048, causal)].name  # 512 blocks
-    # between the KV-quad's and the paired tier's non-causal shapes: the KV-pair
-    assert "_kvpair_" in cfgs[fa.select_config(1, 20, 1024, False)].name
+    # between the KV-quad's and the paired tier's non-causal shapes over long
+    # heads: the KV-pair; shorter heads: one round of pairs
+    assert "_asm_pair_" in cfgs[fa.select_config(1, 20, 1024, False)].name
+    assert "_kvpair_" in cfgs[fa.select_config(1, 5, 4160, False)].name  # long heads (65 blocks)
     # long heads, few of them: causal -> the KV-quad's four-way key split
     # (the _ws entries run the split tier there), non-causal -> the paired tier
     want = "_kvquad_" if causal else "_asm_pair_"
@@ -255,8 +257,8 @@ def test_config_table_ships_only_used_tiers():
     by_name = {c.name: c for c in cfgs}
     used = set()
     for causal in (False, True):
-        for s in (1, 64, 128, 200, 256, 300, 512, 768, 1024, 2048, 4096, 8192, 16384, 32768):
-            for b, h in ((1, 1), (1, 2), (1, 4), (1, 8), (1, 16), (1, 32), (1, 64), (2, 32),
+        for s in (1, 64, 128, 200, 256, 300, 512, 768, 1024, 2048, 4096, 4160, 8192, 16384, 32768):
+            for b, h in ((1, 1), (1, 2), (1, 4), (1, 5), (1, 8), (1, 16), (1, 32), (1, 64), (2, 32),
                          (4, 32), (8, 32), (16, 32), (64, 32), (3, 40), (1, 203), (1, 20)):
                 base = cfgs[fa.select_config(b, h, s, causal)].name
                 used |= {pre + base for pre in TWIN_PREFIXES if pre + base in by_name}
