@@ -14,4 +14,7 @@ for spec in "1 32 1024 --causal" "1 32 2048 --causal --quad"; do
   timeout -k 10 120 python tools/w4p_stamps.py --batch $1 --heads $2 --seq $3 $4 $5 || exit 1
 done 2>&1 | grep -v amdgpu.ids > ../gpurun_out/w4p_stamps.jsonl || exit 1
 timeout -k 10 300 python tools/w4_tail.py --seq 4096 --batch 64 --causal > ../gpurun_out/w4_tail.jsonl || exit 1
+cd ..
+timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+  --master-port 29511 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_torchrun_n1.json 2> gpurun_out/bench_torchrun_n1.err || exit 1
 echo done

@@ -40,6 +40,8 @@ SHAPES = [  # (label, batch, heads, seq, causal[, forced tier name | "auto"])
     ("s512_causal", 1, 32, 512, True),
     ("cfg1_s1024_causal", 1, 32, 1024, True),
     ("s1024_noncausal", 1, 32, 1024, False),
+    ("s768_causal", 1, 32, 768, True),
+    ("s1536_causal", 1, 32, 1536, True),
     ("s2048_causal", 1, 32, 2048, True),
     ("s4096_noncausal", 1, 32, 4096, False),
     ("cfg2_s8192_noncausal", 1, 32, 8192, False),
@@ -61,7 +63,9 @@ SHAPES = [  # (label, batch, heads, seq, causal[, forced tier name | "auto"])
     ("bn128_s8192_noncausal", 1, 32, 8192, False, "bm128_bn128_w4_m16_noncausal"),
     ("bn128_s8192_causal", 1, 32, 8192, True, "bm128_bn128_w4_m16_causal"),
     ("pingpong_item_s8192_causal", 1, 32, 8192, True, "bm256_bn64_w8_m16_pingpong_causal"),
-    # what the round-6 singles replaced at S=512 (the pair grouping, the KV-quad)
+    # what the round-6 singles / mixed / planned groups replaced
+    ("pair_s768_causal", 1, 32, 768, True, "bm128_bn64_w4x32_m16_asm_pair_causal"),
+    ("quad_s1536_causal", 1, 32, 1536, True, "bm256_bn64_w4x64_m16_asm_quad_causal"),
     ("pair_s512_causal", 1, 32, 512, True, "bm128_bn64_w4x32_m16_asm_pair_causal"),
     ("kvquad_cfg0_s512_noncausal", 1, 32, 512, False, "bm64_bn64_w8_m16_kvquad_noncausal"),
     # the KV-pair the round-5 paired / quad tier replaced on short causal launches
